@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""bench.py -- Mpaths/s of the MI355X path-tracing megakernel (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], SURVEY.md 8d "C2"): Cornell box + 10k-tri
+torus knot, diffuse only, 1280x720, 2 paths/pixel/frame, 4 bounces, default
+camera, Fresnel 0.1/3.0.  One "step" = one progressive accumulation step of
+FRAMES_PER_STEP frames over the whole 1280x720 image (inputs resident in
+HBM), ending with the tile gather to rank 0 when N > 1.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F]
+
+N > 1: one process per GPU (torch.distributed.run), 16-row bands dealt
+round-robin, each rank renders its bands of every frame, then one RCCL gather
+(torch.distributed over "nccl" = RCCL) of the RGBA8 tiles to rank 0 per step.
+Strong scaling: the frame size is fixed.
+
+Prints ONE JSON line (rank 0).  value = total paths of all ranks / max-over-
+ranks wall time of the K timed steps.  roofline = the render kernel's
+algorithmic bytes per launch (counted by the kernel's counting variant on a
+separate, untimed step; SURVEY.md 8d byte costs) / its average launch time
+(HIP events on the render stream, inside the timed region).  cpu_baseline =
+the CPU oracle (oracle/, a C restatement of the reference kernel) on a
+bounded sample of the same workload on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CFG = "C2"
+PROFILE_TRAFFIC = os.path.join(REPO, "profiles", "traffic_c2.json")
+
+
+def algorithmic_bytes(c: dict, paths: int, pixel_frames: int) -> float:
+    """64 B/node visit, 16 B/vert0 slot read, +32 B/triangle
+    tested, hit attribute bytes, 16 B/texture or HDRI fetch, 12 B/BRDF lookup,
+    92 B of pixel I/O per pixel-frame."""
+    return (64 * c["node_visits"] + 16 * c["slot_reads"] + 32 * c["tri_tests"] + c["attr_bytes"]
+            + 16 * c["tex_fetches"] + 16 * c["hdr_fetches"] + 12 * c["brdf_fetches"] + 92 * pixel_frames)
+
+
+def cpu_baseline(scene: dict, budget_s: float, threads: int) -> dict:
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import pyoracle
+    pyoracle.build()
+    W, H = scene["width"], scene["height"]
+    accum = np.zeros((H, W, 4), np.float32)
+    rows, t0 = 0, time.perf_counter()
+    chunk = 16
+    while rows < H and time.perf_counter() - t0 < budget_s:
+        r1 = min(H, rows + chunk)
+        pyoracle.render(scene, frames=1, times=[scene["time"]], rows=(rows, r1), threads=threads, accum=accum)
+        rows = r1
+    dt = time.perf_counter() - t0
+    paths = rows * W * 2
+    return {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ C restatement (glibc libm, -O2, OpenMP {threads} threads), frame 1 of C2 "
+                      f"1280x720, rows 0-{rows - 1} ({paths} paths, {dt:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames-per-step", type=int, default=8)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from vrenderer_pathtracer_amd import VRendererHIP, build_native, scenes
+    build_native()
+    scene = scenes.make_scene(CFG)
+    W, H = scene["width"], scene["height"]
+    F = args.frames_per_step
+
+    r = VRendererHIP(local_rank)
+    scenes.load_into(r, scene)
+    stream = torch.cuda.current_stream(dev)
+    r.set_stream(stream.cuda_stream)
+    r.set_tiling(rank, world)
+    owned = r.owned_rows()
+    max_owned = ((H // 16 + world - 1) // world) * 16
+    send = torch.empty(max_owned * W * 4, dtype=torch.uint8, device=dev)
+    gather = [torch.empty_like(send) for _ in range(world)] if (world > 1 and rank == 0) else None
+    recv_flat = torch.empty(world * send.numel(), dtype=torch.uint8, device=dev) if gather is not None else None
+
+    # counting step (untimed): exact event counts for this rank's share
+    counts = r.render_counted(frames=F, time_seed=scene["time"])
+    r.clearBuffer()
+
+    def step(i):
+        times = [scene["time"] + i * F + k for k in range(F)]
+        r.render(frames=F, times=times, sync=False)
+        if world > 1:
+            r.pack_rows(0, send.data_ptr())
+            dist.gather(send, gather, dst=0)
+            if rank == 0:
+                torch.cat(gather, out=recv_flat)
+                r.unpack_rows(0, recv_flat.data_ptr(), world, send.numel())
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    r.kernel_stats(reset=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms, launches = r.kernel_stats()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # aggregate counts over ranks
+    keys = sorted(counts)
+    cvec = torch.tensor([counts[k] for k in keys] + [owned], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(cvec)
+    tot = {k: float(v) for k, v in zip(keys + ["owned_rows"], cvec.tolist())}
+
+    wr = (W // 16) * 16
+    hr = (H // 16) * 16
+    paths_per_step = wr * hr * 2 * F
+    total_paths = paths_per_step * args.steps
+    value = total_paths / elapsed / 1e6
+    rays_per_path = tot["rays"] / paths_per_step
+    mrays = value * rays_per_path
+
+    if rank == 0:
+        # roofline of the render kernel on rank 0 (its own share per launch)
+        own_paths = owned * wr * 2 * F
+        bytes_per_launch = algorithmic_bytes(counts, own_paths, owned * wr * F)
+        avg_launch_s = (kms / 1e3) / max(launches, 1)
+        achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        traffic = None
+        if os.path.exists(PROFILE_TRAFFIC):
+            try:
+                traffic = json.load(open(PROFILE_TRAFFIC)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "Mpaths/sec (+ Mrays/sec) at 1280x720 progressive; 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural Cornell box + 10k-tri torus knot; SURVEY.md 8d C2)",
+            "config": {"workload": "C2: Cornell box + 10k-tri torus knot, diffuse, 1280x720, 2 spp/frame, "
+                                   "4 bounces", "width": W, "height": H, "frames_per_step": F,
+                       "paths_per_step": paths_per_step, "parallelism": f"tile{world}",
+                       "gather": "RCCL gather of RGBA8 bands to rank 0 per step" if world > 1 else "none"},
+            "mrays_per_s": round(mrays, 3),
+            "rays_per_path": round(rays_per_path, 4),
+            "bytes_per_path": round(bytes_per_launch / max(own_paths, 1), 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "render_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "launches": launches},
+        }
+        if not args.no_cpu and world == 1:
+            threads = min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(scene, args.cpu_budget, threads)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    r.cleanUp()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

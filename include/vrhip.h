@@ -1,0 +1,181 @@
+/*
+ * vrhip.h -- C ABI of libvrhip.so, the MI355X (gfx950) path-tracing backend
+ * that drops in behind the reference's vRenderer interface as vRendererHIP.
+ *
+ * Plain C: opaque handle, plain pointers and sizes, int status codes
+ * (0 = VRHIP_OK, never exit()).  All host pointers are copied; the library
+ * never frees caller memory.  Calls on one context are not re-entrant (the
+ * reference runs everything on the Qt GUI thread, src/NGLScene.cpp:249-472).
+ *
+ * Each entry point names the reference interface it replaces.  Reference
+ * paths are relative to the v0q/vRenderer_PathTracer repository root.
+ */
+#ifndef VRHIP_H
+#define VRHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VRHIP_ABI_VERSION 1
+
+typedef enum vrhip_status {
+    VRHIP_OK = 0,
+    VRHIP_ERR_INVALID = -1,      /* bad argument / handle */
+    VRHIP_ERR_HIP = -2,          /* HIP runtime error (see vrhip_last_error) */
+    VRHIP_ERR_NO_ENV = -3,       /* HDRI mode with no environment loaded */
+    VRHIP_ERR_BVH = -4,          /* malformed or too-deep flattened BVH */
+    VRHIP_ERR_NO_DEVICE = -5,
+    VRHIP_ERR_NOMEM = -6
+} vrhip_status;
+
+/* vTextureType, cuda/include/PathTracer.cuh:86 */
+typedef enum vrhip_texture_type { VRHIP_TEX_DIFFUSE = 0, VRHIP_TEX_NORMAL = 1, VRHIP_TEX_SPECULAR = 2 } vrhip_texture_type;
+
+typedef struct vrhip_ctx vrhip_ctx;
+
+/* Thread-local text of the last error. */
+const char *vrhip_last_error(void);
+int vrhip_abi_version(void);
+int vrhip_device_count(int *count);
+
+/* ---- lifetime -------------------------------------------------------- */
+/* replaces vRendererCuda::init (src/vRendererCuda.cpp:38-55): allocates the
+ * float4[W*H] accumulation buffer and the RGBA8 colour/depth images on
+ * `device`, zero-fills, frame counter = 1. */
+int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx **out);
+/* replaces vRendererCuda::cleanUp + cu_cleanUp (src/vRendererCuda.cpp:167-199,
+ * cuda/src/PathTracer.cu:1009-1030). NULL is a no-op. */
+int vrhip_destroy(vrhip_ctx *ctx);
+/* Run subsequent work on this hipStream_t (NULL = the context's own stream). */
+int vrhip_set_stream(vrhip_ctx *ctx, void *hip_stream);
+void *vrhip_get_stream(vrhip_ctx *ctx);
+
+/* ---- per-frame state -------------------------------------------------- */
+/* replaces vRendererCuda::updateCamera (src/vRendererCuda.cpp:69-98): copies
+ * the camera (xyz used, w = 0 as in the reference), resets frame = 1 and
+ * clears the accumulation buffer. */
+int vrhip_set_camera(vrhip_ctx *ctx, const float origin[3], const float dir[3],
+                     const float up[3], const float right[3], float fov_scale);
+/* replaces vRendererCuda::clearBuffer (src/vRendererCuda.cpp:100-105) and
+ * cu_fillFloat4 (cuda/src/PathTracer.cu:1003-1007). */
+int vrhip_clear(vrhip_ctx *ctx);
+/* Stores the Fresnel parameters passed by value to every launch
+ * (include/vRenderer.h:139-145; the base class then calls clearBuffer). */
+int vrhip_set_fresnel(vrhip_ctx *ctx, float coef, float power);
+/* replace cu_useCornellBox / cu_useExampleSphere / cu_useBRDF
+ * (cuda/src/PathTracer.cu:976-989); flags travel by value in the launch. */
+int vrhip_use_cornell_box(vrhip_ctx *ctx, int enable);
+int vrhip_use_example_sphere(vrhip_ctx *ctx, int enable);
+int vrhip_use_brdf(vrhip_ctx *ctx, int enable);
+
+/* ---- scene uploads ---------------------------------------------------- */
+/* replaces the device half of vRendererCuda::initMesh
+ * (src/vRendererCuda.cpp:282-317) + cu_meshInitialised
+ * (cuda/src/PathTracer.cu:997-1001): takes the flattened arrays in exactly
+ * the reference layout (bvh: float4[n_bvh_f4], node = 4 float4 as in
+ * :271-278; verts/normals/tangents: float4[n_slots]; uvs: float2[n_slots];
+ * leaf runs end with a 0x80000000 terminator slot).  The library validates
+ * the tree, records its depth and builds its own device layout. */
+int vrhip_upload_mesh_flat(vrhip_ctx *ctx,
+                           const float *bvh, size_t n_bvh_f4,
+                           const float *verts, const float *normals,
+                           const float *tangents, const float *uvs, size_t n_slots);
+/* Convenience: indexed triangle mesh (vHVert/vHTriangle, include/vDataTypes.h)
+ * -> native binned-SAH BVH -> reference flattening -> upload.  positions,
+ * normals, tangents: float[3*n_verts]; uvs: float[2*n_verts] (may be NULL);
+ * tris: uint32[3*n_tris]. */
+int vrhip_upload_mesh_indexed(vrhip_ctx *ctx, const float *positions, const float *normals,
+                              const float *tangents, const float *uvs, uint32_t n_verts,
+                              const uint32_t *tris, uint32_t n_tris, uint32_t max_leaf_tris);
+/* replaces vRendererCuda::loadHDR (src/vRendererCuda.cpp:320-340) +
+ * cu_setHDRDim: rgba float4[w*h] (or half4 with the _half variant, the
+ * Imf::Rgba layout, converted on the device). */
+int vrhip_upload_hdr(vrhip_ctx *ctx, const float *rgba, uint32_t w, uint32_t h);
+int vrhip_upload_hdr_half(vrhip_ctx *ctx, const uint16_t *rgba_half, uint32_t w, uint32_t h);
+/* replaces the device half of vRendererCuda::loadTexture
+ * (src/vRendererCuda.cpp:342-411) + cu_bindTexture: rgba float4[w*h]
+ * (already gamma-converted by the caller, as the reference host does). */
+int vrhip_upload_texture(vrhip_ctx *ctx, int type, const float *rgba, uint32_t w, uint32_t h);
+/* replaces the device half of vRendererCuda::loadBRDF
+ * (src/vRendererCuda.cpp:413-437) + cu_bindBRDF: float[3*90*90*180] planar
+ * R,G,B MERL table.  Copies; does NOT take ownership (the C++ adapter
+ * reproduces the reference's delete[]). */
+int vrhip_upload_brdf(vrhip_ctx *ctx, const float *table, size_t n_floats);
+
+/* ---- rendering -------------------------------------------------------- */
+/* replaces vRendererCuda::render (src/vRendererCuda.cpp:107-165) +
+ * cu_runRenderKernel (cuda/src/PathTracer.cu:870-892), for n_frames
+ * consecutive frames in one device pass.  times[i] is the _time RNG seed of
+ * frame i (the reference uses wall-clock ms); times may be NULL, then
+ * `time_seed` is used for every frame.  Enqueues on the context stream and
+ * returns; call vrhip_sync for the reference's synchronous behaviour. */
+int vrhip_render(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed);
+/* Same render, through the counting kernel variant (identical results, plus
+ * per-event counts for the roofline's algorithmic bytes):
+ * counters[0..7] = rays (intersectScene calls), inner-node visits (64 B),
+ * vert0 slot reads incl. terminators (16 B), triangle tests (+32 B), hit
+ * attribute bytes, texture fetches (16 B), HDRI fetches (16 B), BRDF lookups
+ * (12 B).  Synchronous. */
+int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
+                         uint64_t counters[8]);
+int vrhip_sync(vrhip_ctx *ctx);
+/* Frames rendered since the last clear (vRendererCuda::getFrameCount,
+ * include/vRendererCuda.h:124). */
+int vrhip_frame_count(vrhip_ctx *ctx, uint32_t *frames);
+
+/* ---- read-back -------------------------------------------------------- */
+int vrhip_read_accum(vrhip_ctx *ctx, float *out_rgba_f32);       /* float4[W*H] */
+int vrhip_read_rgba8(vrhip_ctx *ctx, uint8_t *out_rgba8);        /* uchar4[W*H] */
+int vrhip_read_depth8(vrhip_ctx *ctx, uint8_t *out_rgba8);       /* uchar4[W*H] */
+/* Device pointers of the resident buffers (for GL interop / RCCL gather). */
+int vrhip_device_buffers(vrhip_ctx *ctx, void **accum, void **rgba8, void **depth8);
+
+/* ---- multi-GPU image-tile sharding ------------------------------------ */
+/* Render only 16-row bands b with b % n_ranks == rank (interleaved for load
+ * balance).  Seeds use global pixel coordinates, so the union of the ranks'
+ * bands equals the 1-GPU image bit for bit. */
+int vrhip_set_tiling(vrhip_ctx *ctx, uint32_t rank, uint32_t n_ranks);
+/* Number of rows this rank owns in the rendered region. */
+int vrhip_owned_rows(vrhip_ctx *ctx, uint32_t *rows);
+/* Pack this rank's owned rows (RGBA8 if what == 0, float4 accum if 1,
+ * depth8 if 2) contiguously into dst (device pointer), in band order. */
+int vrhip_pack_rows(vrhip_ctx *ctx, int what, void *dst_device);
+/* On the gathering rank: scatter n_ranks packed buffers from src (device;
+ * rank r's buffer starts at r * stride_bytes, stride_bytes = 0 means
+ * tightly packed) into this context's full image `what`. */
+int vrhip_unpack_rows(vrhip_ctx *ctx, int what, const void *src_device, uint32_t n_ranks, size_t stride_bytes);
+
+/* ---- diagnostics ------------------------------------------------------ */
+/* Kernel time of the last vrhip_render (ms, HIP events on the context stream;
+ * requires vrhip_sync first). */
+int vrhip_last_kernel_ms(vrhip_ctx *ctx, float *ms);
+/* Accumulated render-kernel time (ms) and launch count since the last reset,
+ * from HIP events recorded around every vrhip_render on the context stream. */
+int vrhip_kernel_stats(vrhip_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
+/* Depth of the uploaded BVH and the traversal stack size in use. */
+int vrhip_bvh_info(vrhip_ctx *ctx, uint32_t *depth, uint32_t *n_nodes, uint32_t *n_slots);
+/* Evaluate the device libm on n inputs (test hook: 0 sin, 1 cos, 2 acos,
+ * 3 atan2, 4 pow, 5 fmin, 6 fmax, 7 f2i); a,b,out host arrays of n floats. */
+int vrhip_selftest_math(int device, int fn, const float *a, const float *b, float *out, size_t n);
+
+/* ---- host-side helpers (no device needed) ----------------------------- */
+/* Native BVH build + reference flattening (src/vRendererCuda.cpp:204-279)
+ * into caller arrays.  Call once with NULL outputs to get the sizes. */
+int vrhip_build_flat(const float *positions, const float *normals, const float *tangents,
+                     const float *uvs, uint32_t n_verts, const uint32_t *tris, uint32_t n_tris,
+                     uint32_t max_leaf_tris,
+                     float *bvh_out, size_t *n_bvh_f4,
+                     float *verts_out, float *normals_out, float *tangents_out, float *uvs_out,
+                     size_t *n_slots);
+/* Check a flattened tree; returns VRHIP_OK and its depth / inner-node count. */
+int vrhip_validate_flat(const float *bvh, size_t n_bvh_f4, const float *verts, size_t n_slots,
+                        uint32_t *depth, uint32_t *n_nodes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VRHIP_H */

@@ -1,0 +1,115 @@
+"""ctypes binding of libvrhip.so (the C ABI in include/vrhip.h).
+
+There is no fallback: if the HIP library is missing or fails to load, every
+entry point raises.  torch is imported first when available so that the
+process shares ONE HIP runtime (torch ships its own libamdhip64 with the same
+soname; loading ours first would pull in a second copy).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+from . import build as _build
+
+try:  # share torch's HIP runtime if torch is in use
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the C ABI
+    torch = None
+
+_f = ctypes.POINTER(ctypes.c_float)
+_u8 = ctypes.POINTER(ctypes.c_uint8)
+_u16 = ctypes.POINTER(ctypes.c_uint16)
+_u32 = ctypes.POINTER(ctypes.c_uint32)
+_sz = ctypes.POINTER(ctypes.c_size_t)
+_vp = ctypes.c_void_p
+_ctx = ctypes.c_void_p
+
+VRHIP_OK = 0
+ERRORS = {-1: "VRHIP_ERR_INVALID", -2: "VRHIP_ERR_HIP", -3: "VRHIP_ERR_NO_ENV", -4: "VRHIP_ERR_BVH",
+          -5: "VRHIP_ERR_NO_DEVICE", -6: "VRHIP_ERR_NOMEM"}
+
+_SIGNATURES = {
+    "vrhip_last_error": (ctypes.c_char_p, []),
+    "vrhip_abi_version": (ctypes.c_int, []),
+    "vrhip_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "vrhip_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_ctx)]),
+    "vrhip_destroy": (ctypes.c_int, [_ctx]),
+    "vrhip_set_stream": (ctypes.c_int, [_ctx, _vp]),
+    "vrhip_get_stream": (_vp, [_ctx]),
+    "vrhip_set_camera": (ctypes.c_int, [_ctx, _f, _f, _f, _f, ctypes.c_float]),
+    "vrhip_clear": (ctypes.c_int, [_ctx]),
+    "vrhip_set_fresnel": (ctypes.c_int, [_ctx, ctypes.c_float, ctypes.c_float]),
+    "vrhip_use_cornell_box": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "vrhip_use_example_sphere": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "vrhip_use_brdf": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "vrhip_upload_mesh_flat": (ctypes.c_int, [_ctx, _f, ctypes.c_size_t, _f, _f, _f, _f, ctypes.c_size_t]),
+    "vrhip_upload_mesh_indexed": (ctypes.c_int, [_ctx, _f, _f, _f, _f, ctypes.c_uint32, _u32, ctypes.c_uint32,
+                                                 ctypes.c_uint32]),
+    "vrhip_upload_hdr": (ctypes.c_int, [_ctx, _f, ctypes.c_uint32, ctypes.c_uint32]),
+    "vrhip_upload_hdr_half": (ctypes.c_int, [_ctx, _u16, ctypes.c_uint32, ctypes.c_uint32]),
+    "vrhip_upload_texture": (ctypes.c_int, [_ctx, ctypes.c_int, _f, ctypes.c_uint32, ctypes.c_uint32]),
+    "vrhip_upload_brdf": (ctypes.c_int, [_ctx, _f, ctypes.c_size_t]),
+    "vrhip_render": (ctypes.c_int, [_ctx, ctypes.c_uint32, _u32, ctypes.c_uint32]),
+    "vrhip_render_counted": (ctypes.c_int, [_ctx, ctypes.c_uint32, _u32, ctypes.c_uint32,
+                                            ctypes.POINTER(ctypes.c_uint64)]),
+    "vrhip_kernel_stats": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.c_int]),
+    "vrhip_sync": (ctypes.c_int, [_ctx]),
+    "vrhip_frame_count": (ctypes.c_int, [_ctx, _u32]),
+    "vrhip_read_accum": (ctypes.c_int, [_ctx, _f]),
+    "vrhip_read_rgba8": (ctypes.c_int, [_ctx, _u8]),
+    "vrhip_read_depth8": (ctypes.c_int, [_ctx, _u8]),
+    "vrhip_device_buffers": (ctypes.c_int, [_ctx, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
+    "vrhip_set_tiling": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32]),
+    "vrhip_owned_rows": (ctypes.c_int, [_ctx, _u32]),
+    "vrhip_pack_rows": (ctypes.c_int, [_ctx, ctypes.c_int, _vp]),
+    "vrhip_unpack_rows": (ctypes.c_int, [_ctx, ctypes.c_int, _vp, ctypes.c_uint32, ctypes.c_size_t]),
+    "vrhip_last_kernel_ms": (ctypes.c_int, [_ctx, _f]),
+    "vrhip_bvh_info": (ctypes.c_int, [_ctx, _u32, _u32, _u32]),
+    "vrhip_selftest_math": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _f, _f, _f, ctypes.c_size_t]),
+    "vrhip_build_flat": (ctypes.c_int, [_f, _f, _f, _f, ctypes.c_uint32, _u32, ctypes.c_uint32, ctypes.c_uint32,
+                                        _f, _sz, _f, _f, _f, _f, _sz]),
+    "vrhip_validate_flat": (ctypes.c_int, [_f, ctypes.c_size_t, _f, ctypes.c_size_t, _u32, _u32]),
+}
+
+_lib = None
+
+
+class VRHIPError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where}: {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/vrhip.h."""
+    hdr = os.path.join(_build.REPO_DIR, "include", "vrhip.h")
+    text = open(hdr).read()
+    return sorted(set(re.findall(r"\b(vrhip_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = _build.LIB_PATH
+        if not os.path.exists(path):
+            raise RuntimeError(f"libvrhip.so not built ({path}); run vrenderer_pathtracer_amd.build.build()")
+        L = ctypes.CDLL(path)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(code: int, where: str) -> None:
+    if code != VRHIP_OK:
+        msg = lib().vrhip_last_error()
+        raise VRHIPError(code, where, msg.decode() if msg else "")
+
+
+def fptr(a):
+    return None if a is None else a.ctypes.data_as(_f)

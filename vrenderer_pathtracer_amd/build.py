@@ -1,0 +1,61 @@
+"""Build the native backend in-tree: libvrhip.so (HIP, gfx950) via hipcc.
+
+The product is a C-ABI shared library (include/vrhip.h); Python only loads it
+with ctypes.  Built in-tree so it travels with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libvrhip.so")
+SOURCES = ["vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp"]
+HEADERS = ["vr_params.hpp", "vr_math.hpp", "vr_bvh.hpp"]
+ARCH = os.environ.get("VRHIP_OFFLOAD_ARCH", "gfx950")
+
+# -ffp-contract=off: results are defined without FMA contraction (parity
+# with the CPU oracle); division and sqrt stay IEEE (hipcc default).
+HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
+               f"--offload-arch={ARCH}"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: cannot build libvrhip.so")
+
+
+def _newest_input_mtime() -> float:
+    paths = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    paths.append(os.path.join(REPO_DIR, "include", "vrhip.h"))
+    paths.append(os.path.abspath(__file__))
+    return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
+
+
+def needs_build() -> bool:
+    return not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < _newest_input_mtime()
+
+
+def build(force: bool = False, verbose: bool = False, extra_flags=None) -> str:
+    if not force and not needs_build():
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [_hipcc()] + HIPCC_FLAGS + list(extra_flags or []) + ["-o", tmp] + \
+          [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + res.stdout + res.stderr)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

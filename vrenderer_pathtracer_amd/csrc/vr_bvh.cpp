@@ -1,0 +1,267 @@
+// vr_bvh.cpp -- host BVH builder + flattener for libvrhip.
+//
+// The reference builds an SBVH on the host (src/SBVH.cpp:15-569, leaves of
+// <= kMinLeafSize = 4 triangles, include/Utilities.h:16-21) and flattens it
+// in vRendererCuda::initMesh (src/vRendererCuda.cpp:204-279).  The kernel's
+// closest hit does not depend on the tree shape (no t-culling in the
+// reference traversal, PathTracer.cu:316,322), so any valid tree renders the
+// same image; this file builds a binned-SAH tree (object splits, 32 bins per
+// axis, SAH costs kNodeCost = kTriangleCost = 1 as in the reference) and
+// writes it in exactly the reference's flattened layout:
+//   node (4 float4): (c0.minx,c0.maxx,c0.miny,c0.maxy) (c1.minx,c1.maxx,c1.miny,c1.maxy)
+//                    (c0.minz,c0.maxz,c1.minz,c1.maxz) (bits(idx0),bits(idx1),0,0)
+//   idx >= 0: float4 offset of an inner child; idx < 0: ~first slot of a leaf
+//   leaf run: 3 slots per triangle, then one terminator slot (x bits 0x80000000).
+#include "vr_bvh.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+namespace vr {
+namespace {
+
+struct Box {
+    float lo[3] = { std::numeric_limits<float>::infinity(), std::numeric_limits<float>::infinity(),
+                    std::numeric_limits<float>::infinity() };
+    float hi[3] = { -std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity(),
+                    -std::numeric_limits<float>::infinity() };
+    void grow(const float* p) {
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], p[a]); hi[a] = std::max(hi[a], p[a]); }
+    }
+    void grow(const Box& b) {
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], b.lo[a]); hi[a] = std::max(hi[a], b.hi[a]); }
+    }
+    bool empty() const { return lo[0] > hi[0]; }
+    double area() const {
+        if (empty()) return 0.0;
+        const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct BuildNode {
+    Box box;
+    int child[2] = { -1, -1 };
+    uint32_t first = 0, count = 0;   // leaf range into the reference index list
+    bool leaf = false;
+};
+
+struct Builder {
+    const float* pos;
+    const uint32_t* tris;
+    uint32_t max_leaf;
+    uint32_t max_depth;
+    std::vector<Box> tri_box;
+    std::vector<float> centroid;       // 3 per triangle
+    std::vector<uint32_t> refs;        // triangle references (leaf ranges index this)
+    std::vector<BuildNode> nodes;
+
+    static constexpr int kBins = 32;
+
+    int make_leaf(uint32_t first, uint32_t count, const Box& b) {
+        BuildNode n; n.box = b; n.first = first; n.count = count; n.leaf = true;
+        nodes.push_back(n);
+        return (int)nodes.size() - 1;
+    }
+
+    // Returns node index.  force_split: the root must be an inner node (the
+    // flattened layout stores leaves inside their parent).
+    int build(uint32_t first, uint32_t count, uint32_t depth, bool force_split) {
+        Box b, cb;
+        for (uint32_t i = first; i < first + count; ++i) {
+            b.grow(tri_box[refs[i]]);
+            cb.grow(&centroid[3 * refs[i]]);
+        }
+        if (!force_split && (count <= 1 || depth + 1 >= max_depth)) return make_leaf(first, count, b);
+
+        // binned SAH over centroids
+        double best_cost = std::numeric_limits<double>::infinity();
+        int best_axis = -1, best_split = -1;
+        for (int a = 0; a < 3; ++a) {
+            const float ext = cb.hi[a] - cb.lo[a];
+            if (!(ext > 0.f)) continue;
+            Box bin_box[kBins];
+            uint32_t bin_cnt[kBins] = {};
+            const double scale = kBins / (double)ext;
+            for (uint32_t i = first; i < first + count; ++i) {
+                const uint32_t t = refs[i];
+                int k = (int)(((double)centroid[3 * t + a] - cb.lo[a]) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                bin_cnt[k]++;
+                bin_box[k].grow(tri_box[t]);
+            }
+            double right_area[kBins];
+            uint32_t right_cnt[kBins];
+            Box acc; uint32_t c = 0;
+            for (int k = kBins - 1; k > 0; --k) {
+                acc.grow(bin_box[k]); c += bin_cnt[k];
+                right_area[k] = acc.area(); right_cnt[k] = c;
+            }
+            acc = Box(); c = 0;
+            for (int k = 0; k < kBins - 1; ++k) {
+                acc.grow(bin_box[k]); c += bin_cnt[k];
+                if (c == 0 || right_cnt[k + 1] == 0) continue;
+                const double cost = acc.area() * c + right_area[k + 1] * right_cnt[k + 1];
+                if (cost < best_cost) { best_cost = cost; best_axis = a; best_split = k; }
+            }
+        }
+        const double parent_area = b.area();
+        // SAH: C_node + (A_L N_L + A_R N_R) / A_P * C_tri  vs  N * C_tri
+        const double split_cost = 1.0 + (parent_area > 0.0 ? best_cost / parent_area : (double)count);
+        const bool want_leaf = count <= max_leaf && (best_axis < 0 || split_cost >= (double)count);
+        if (!force_split && want_leaf) return make_leaf(first, count, b);
+
+        uint32_t mid;
+        if (best_axis >= 0) {
+            const int a = best_axis;
+            const double scale = kBins / (double)(cb.hi[a] - cb.lo[a]);
+            auto it = std::partition(refs.begin() + first, refs.begin() + first + count, [&](uint32_t t) {
+                int k = (int)(((double)centroid[3 * t + a] - cb.lo[a]) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                return k <= best_split;
+            });
+            mid = (uint32_t)(it - refs.begin());
+        } else {
+            mid = first + count / 2;          // coincident centroids: median by index
+        }
+        if (mid == first || mid == first + count) mid = first + count / 2;
+
+        int left, right;
+        if (count == 1) {
+            // a single triangle under a forced split: duplicate the reference
+            // (the second test ties at equal t and the strict < keeps the first)
+            left = make_leaf(first, 1, b);
+            right = make_leaf(first, 1, b);
+        } else {
+            left = build(first, mid - first, depth + 1, false);
+            right = build(mid, first + count - mid, depth + 1, false);
+        }
+        BuildNode n; n.box = b; n.child[0] = left; n.child[1] = right; n.leaf = false;
+        nodes.push_back(n);
+        return (int)nodes.size() - 1;
+    }
+};
+
+inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+inline int32_t fbits(float f) { int32_t i; std::memcpy(&i, &f, 4); return i; }
+
+} // namespace
+
+int build_flat(const float* positions, const float* normals, const float* tangents, const float* uvs,
+               uint32_t n_verts, const uint32_t* tris, uint32_t n_tris, uint32_t max_leaf_tris,
+               FlatMesh& out)
+{
+    if (!positions || !tris || n_tris == 0 || n_verts == 0) return -1;
+    for (uint32_t i = 0; i < 3 * n_tris; ++i)
+        if (tris[i] >= n_verts) return -1;
+    Builder B;
+    B.pos = positions; B.tris = tris;
+    B.max_leaf = max_leaf_tris ? max_leaf_tris : 4;
+    B.max_depth = kMaxBuildDepth;
+    B.tri_box.resize(n_tris);
+    B.centroid.resize(3 * (size_t)n_tris);
+    B.refs.resize(n_tris);
+    for (uint32_t t = 0; t < n_tris; ++t) {
+        Box bx;
+        for (int k = 0; k < 3; ++k) bx.grow(&positions[3 * (size_t)tris[3 * t + k]]);
+        B.tri_box[t] = bx;
+        for (int a = 0; a < 3; ++a) B.centroid[3 * (size_t)t + a] = 0.5f * (bx.lo[a] + bx.hi[a]);
+        B.refs[t] = t;
+    }
+    B.nodes.reserve(2 * (size_t)n_tris + 2);
+    const int root = B.build(0, n_tris, 0, true);
+
+    // Flatten (reference: explicit-stack DFS, src/vRendererCuda.cpp:204-279)
+    out.bvh.assign(4, vr4{ 0.f, 0.f, 0.f, 0.f });
+    out.verts.clear(); out.normals.clear(); out.tangents.clear(); out.uvs.clear();
+    std::vector<std::pair<int, uint32_t>> stack{ { root, 0u } };
+    const float term = ibits((int32_t)0x80000000);
+    while (!stack.empty()) {
+        const int ni = stack.back().first;
+        const uint32_t idx = stack.back().second;
+        stack.pop_back();
+        const BuildNode& node = B.nodes[(size_t)ni];
+        int32_t indices[2];
+        for (int i = 0; i < 2; ++i) {
+            const BuildNode& ch = B.nodes[(size_t)node.child[i]];
+            if (!ch.leaf) {
+                const uint32_t cidx = (uint32_t)out.bvh.size();
+                indices[i] = (int32_t)cidx;
+                stack.push_back({ node.child[i], cidx });
+                out.bvh.resize(out.bvh.size() + 4, vr4{ 0.f, 0.f, 0.f, 0.f });
+                continue;
+            }
+            indices[i] = ~(int32_t)out.verts.size();
+            for (uint32_t j = ch.first; j < ch.first + ch.count; ++j) {
+                const uint32_t t = B.refs[j];
+                for (int k = 0; k < 3; ++k) {
+                    const size_t v = tris[3 * (size_t)t + k];
+                    out.verts.push_back(vr4{ positions[3 * v], positions[3 * v + 1], positions[3 * v + 2], 0.f });
+                    if (normals) out.normals.push_back(vr4{ normals[3 * v], normals[3 * v + 1], normals[3 * v + 2], 0.f });
+                    else out.normals.push_back(vr4{ 0.f, 0.f, 0.f, 0.f });
+                    if (tangents) out.tangents.push_back(vr4{ tangents[3 * v], tangents[3 * v + 1], tangents[3 * v + 2], 0.f });
+                    else out.tangents.push_back(vr4{ 0.f, 0.f, 0.f, 0.f });
+                    if (uvs) out.uvs.push_back(vr2{ uvs[2 * v], uvs[2 * v + 1] });
+                    else out.uvs.push_back(vr2{ 0.f, 0.f });
+                }
+            }
+            out.verts.push_back(vr4{ term, 0.f, 0.f, 0.f });
+            out.tangents.push_back(vr4{ term, 0.f, 0.f, 0.f });
+            out.normals.push_back(vr4{ term, 0.f, 0.f, 0.f });
+            out.uvs.push_back(vr2{ term, 0.f });
+        }
+        const Box& b0 = B.nodes[(size_t)node.child[0]].box;
+        const Box& b1 = B.nodes[(size_t)node.child[1]].box;
+        out.bvh[idx + 0] = vr4{ b0.lo[0], b0.hi[0], b0.lo[1], b0.hi[1] };
+        out.bvh[idx + 1] = vr4{ b1.lo[0], b1.hi[0], b1.lo[1], b1.hi[1] };
+        out.bvh[idx + 2] = vr4{ b0.lo[2], b0.hi[2], b1.lo[2], b1.hi[2] };
+        out.bvh[idx + 3] = vr4{ ibits(indices[0]), ibits(indices[1]), 0.f, 0.f };
+    }
+    return 0;
+}
+
+int validate_flat(const float* bvh, size_t n_bvh_f4, const float* verts, size_t n_slots,
+                  uint32_t* depth_out, uint32_t* n_nodes_out)
+{
+    if (!bvh || n_bvh_f4 < 4 || (n_bvh_f4 % 4) != 0 || !verts || n_slots == 0) return -1;
+    const size_t n_nodes = n_bvh_f4 / 4;
+    std::vector<uint8_t> seen(n_nodes, 0);
+    std::vector<std::pair<size_t, uint32_t>> st{ { 0, 1 } };   // (node float4 offset, depth)
+    uint32_t max_depth = 0, count = 0;
+    while (!st.empty()) {
+        const size_t off = st.back().first;
+        const uint32_t d = st.back().second;
+        st.pop_back();
+        if (off % 4 != 0 || off + 4 > n_bvh_f4) return -2;
+        if (seen[off / 4]) return -3;                            // DAG / cycle
+        seen[off / 4] = 1;
+        ++count;
+        max_depth = std::max(max_depth, d);
+        if (d > 255) return -4;
+        const float* n = bvh + 4 * off;
+        for (int c = 0; c < 2; ++c) {
+            const float fv = n[12 + c];
+            const int32_t idx = fbits(fv);
+            if (idx >= 0) {
+                st.push_back({ (size_t)idx, d + 1 });
+            } else {
+                size_t s = (size_t)(~idx);
+                // leaf run: triples until the terminator
+                for (;;) {
+                    if (s >= n_slots) return -5;
+                    if ((uint32_t)fbits(verts[4 * s]) == 0x80000000u) break;
+                    if (s + 3 > n_slots) return -5;
+                    s += 3;
+                }
+            }
+        }
+    }
+    if (depth_out) *depth_out = max_depth;
+    if (n_nodes_out) *n_nodes_out = count;
+    return 0;
+}
+
+} // namespace vr

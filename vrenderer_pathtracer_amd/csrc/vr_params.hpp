@@ -1,0 +1,64 @@
+// vr_params.hpp -- launch parameters shared by the host API (vrhip_api.cpp)
+// and the gfx950 kernels (vr_kernel.hip).  Plain C++ types only.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace vr {
+
+// float4 / float2 with the reference's memory layout (16 B / 8 B aligned)
+struct alignas(16) vr4 { float x, y, z, w; };
+struct alignas(8) vr2 { float x, y; };
+struct alignas(4) u8x4 { unsigned char x, y, z, w; };
+
+enum Flags : uint32_t {
+    F_CORNELL = 1u << 0,     // kUseCornellBox      (PathTracer.cu:32)
+    F_EXAMPLE = 1u << 1,     // kUseExampleSphere   (:30)
+    F_VIEW_BRDF = 1u << 2,   // kViewBRDF           (:31)
+    F_MESH = 1u << 3,        // kMeshInitialised    (:29)
+    F_BRDF = 1u << 4,        // kHasBRDF            (:28)
+    F_TEX_DIFF = 1u << 5,    // kHasDiffuseMap      (:25)
+    F_TEX_NORM = 1u << 6,    // kHasNormalMap       (:26)
+    F_TEX_SPEC = 1u << 7,    // kHasSpecularMap     (:27)
+};
+
+constexpr int kMaxFramesPerLaunch = 64;
+// counting variant: rays, node visits, vert0 slot reads, triangle tests,
+// attribute bytes, texture fetches, HDRI fetches, BRDF lookups
+constexpr int kCounters = 8;
+constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
+constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
+
+struct RenderParams {
+    vr4 cam_o, cam_d, cx, cy;        // cx, cy precomputed exactly as PathTracer.cu:833-836
+    uint32_t W, H, wr, hr;           // wr/hr: rendered region (grid truncation, :888-889)
+    float fresnel_coef, fresnel_pow;
+    uint32_t flags;
+    uint32_t tiles_x;                // wr / 16
+    uint32_t rank, nranks;           // interleaved 16-row band sharding
+    uint32_t first_frame, n_frames;
+    const vr4* bvh;
+    const vr4* verts;
+    const vr4* normals;
+    const vr4* tangents;
+    const vr2* uvs;
+    const vr4* hdr;
+    uint32_t hdr_w, hdr_h;
+    const vr4* tex[3];
+    uint32_t tex_w[3], tex_h[3];
+    const float* brdf;
+    vr4* accum;
+    u8x4* rgba;
+    u8x4* depth;
+    unsigned long long* counters;    // kCounters entries (counting variant only)
+    uint32_t times[kMaxFramesPerLaunch];
+};
+
+// host-side launchers implemented in vr_kernel.hip
+int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream);
+int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);
+int launch_pack_rows(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t hr,
+                     uint32_t rank, uint32_t nranks, int unpack, void* stream);
+int launch_selftest_math(int fn, const float* a, const float* b, float* out, size_t n, void* stream);
+
+} // namespace vr

@@ -1,0 +1,549 @@
+// vrhip_api.cpp -- C ABI of libvrhip.so (declared in include/vrhip.h).
+//
+// Host half of the MI355X backend: the device-side counterpart of
+// vRendererCuda (src/vRendererCuda.cpp) and the cu_* device ABI
+// (cuda/include/PathTracer.cuh:107-165), re-designed around one context per
+// GPU, status codes instead of exit(0) (src/vRendererCuda.cpp:454-467), flags
+// passed by value in the launch instead of __constant__ symbol copies
+// (cuda/src/PathTracer.cu:976-1001), and multi-frame render steps.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vrhip.h"
+#include "vr_bvh.hpp"
+#include "vr_params.hpp"
+
+using vr::vr2;
+using vr::vr4;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) { g_last_error = msg; return code; }
+
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            return fail(VRHIP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));       \
+    } while (0)
+
+template <typename T>
+void dfree(T*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } }
+
+} // namespace
+
+struct vrhip_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t W = 0, H = 0;
+    vr4* accum = nullptr;
+    vr::u8x4* rgba = nullptr;
+    vr::u8x4* depth = nullptr;
+    // camera (vCamera, cuda/include/PathTracer.cuh:58-84)
+    float cam_o[3] = { 0.f, 0.f, 150.f }, cam_d[3] = { 0.f, 0.f, -1.f };
+    float cam_up[3] = { 0.f, 1.f, 0.f }, cam_right[3] = { 1.f, 0.f, 0.f };
+    float fov_scale = 0.f;
+    uint32_t frame = 1;                         // m_frame (src/vRendererCuda.cpp:24)
+    float fresnel_coef = 0.1f, fresnel_pow = 3.f; // src/vRendererCuda.cpp:27-28
+    bool cornell = false, example = false, view_brdf = false;
+    // mesh
+    vr4* bvh = nullptr; vr4* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
+    size_t n_bvh = 0, n_slots = 0;
+    uint32_t bvh_depth = 0, bvh_nodes = 0;
+    bool mesh = false;
+    // environment / textures / brdf
+    vr4* hdr = nullptr; uint32_t hdr_w = 0, hdr_h = 0;
+    vr4* tex[3] = { nullptr, nullptr, nullptr }; uint32_t tex_w[3] = { 0, 0, 0 }, tex_h[3] = { 0, 0, 0 };
+    float* brdf = nullptr;
+    // sharding
+    uint32_t rank = 0, nranks = 1;
+    // timing
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;          // ev0/ev1 hold the last render
+    bool pending = false;        // last render's time not yet added to the totals
+    double kernel_ms_total = 0.0;
+    uint64_t launches_total = 0, launches_pending = 0;
+    unsigned long long* counters = nullptr;
+};
+
+namespace {
+
+// Reference default camera fov: Camera::getFovScale (src/Camera.cpp:4,119-123)
+float default_fov_scale()
+{
+    const float kDegInRad = (float)(M_PI / 180.f);
+    const float fovRad = 75.f * kDegInRad;
+    return std::tan(fovRad / 2.f);
+}
+
+int set_device(vrhip_ctx* c) { HIP_TRY(hipSetDevice(c->device)); return VRHIP_OK; }
+
+int clear_accum(vrhip_ctx* c)
+{
+    c->frame = 1;
+    HIP_TRY(hipMemsetAsync(c->accum, 0, sizeof(vr4) * (size_t)c->W * c->H, c->stream));
+    return VRHIP_OK;
+}
+
+uint32_t rendered_rows(const vrhip_ctx* c) { return (c->H / 16u) * 16u; }
+
+uint32_t owned_rows_of(const vrhip_ctx* c, uint32_t rank)
+{
+    const uint32_t bands = c->H / 16u;
+    const uint32_t owned = bands > rank ? (bands - rank + c->nranks - 1) / c->nranks : 0;
+    return owned * 16u;
+}
+
+template <typename T>
+int upload(vrhip_ctx* c, T*& dst, const void* src, size_t bytes)
+{
+    dfree(dst);
+    HIP_TRY(hipMalloc((void**)&dst, bytes ? bytes : 16));
+    if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return VRHIP_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+const char* vrhip_last_error(void) { return g_last_error.c_str(); }
+int vrhip_abi_version(void) { return VRHIP_ABI_VERSION; }
+
+int vrhip_device_count(int* count)
+{
+    if (!count) return fail(VRHIP_ERR_INVALID, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *count = 0; return fail(VRHIP_ERR_NO_DEVICE, hipGetErrorString(e)); }
+    *count = n;
+    return VRHIP_OK;
+}
+
+int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
+{
+    if (!out || width == 0 || height == 0) return fail(VRHIP_ERR_INVALID, "bad create arguments");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(VRHIP_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= n) return fail(VRHIP_ERR_INVALID, "device index out of range");
+    vrhip_ctx* c = new vrhip_ctx();
+    c->device = device;
+    c->W = width; c->H = height;
+    c->fov_scale = default_fov_scale();
+    int rc;
+    if ((rc = set_device(c)) != VRHIP_OK) { delete c; return rc; }
+    auto cleanup = [&](int code) { vrhip_destroy(c); return code; };
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(VRHIP_ERR_HIP, "hipStreamCreate failed"));
+    c->stream = c->own_stream;
+    const size_t npx = (size_t)width * height;
+    if (hipMalloc((void**)&c->accum, sizeof(vr4) * npx) != hipSuccess ||
+        hipMalloc((void**)&c->rgba, 4 * npx) != hipSuccess ||
+        hipMalloc((void**)&c->depth, 4 * npx) != hipSuccess)
+        return cleanup(fail(VRHIP_ERR_NOMEM, "hipMalloc of frame buffers failed"));
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
+        return cleanup(fail(VRHIP_ERR_HIP, "hipEventCreate failed"));
+    if (hipMemsetAsync(c->rgba, 0, 4 * npx, c->stream) != hipSuccess ||
+        hipMemsetAsync(c->depth, 0, 4 * npx, c->stream) != hipSuccess)
+        return cleanup(fail(VRHIP_ERR_HIP, "hipMemset failed"));
+    if ((rc = clear_accum(c)) != VRHIP_OK) return cleanup(rc);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return cleanup(fail(VRHIP_ERR_HIP, "sync failed"));
+    *out = c;
+    return VRHIP_OK;
+}
+
+int vrhip_destroy(vrhip_ctx* c)
+{
+    if (!c) return VRHIP_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    dfree(c->accum); dfree(c->rgba); dfree(c->depth);
+    dfree(c->bvh); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
+    dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
+    dfree(c->counters);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return VRHIP_OK;
+}
+
+int vrhip_set_stream(vrhip_ctx* c, void* s)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return VRHIP_OK;
+}
+
+void* vrhip_get_stream(vrhip_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int vrhip_set_camera(vrhip_ctx* c, const float origin[3], const float dir[3], const float up[3],
+                     const float right[3], float fov_scale)
+{
+    if (!c || !origin || !dir || !up || !right) return fail(VRHIP_ERR_INVALID, "bad camera arguments");
+    std::memcpy(c->cam_o, origin, 12); std::memcpy(c->cam_d, dir, 12);
+    std::memcpy(c->cam_up, up, 12); std::memcpy(c->cam_right, right, 12);
+    c->fov_scale = fov_scale;
+    int rc = set_device(c); if (rc) return rc;
+    return clear_accum(c);
+}
+
+int vrhip_clear(vrhip_ctx* c)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    int rc = set_device(c); if (rc) return rc;
+    return clear_accum(c);
+}
+
+int vrhip_set_fresnel(vrhip_ctx* c, float coef, float power)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    c->fresnel_coef = coef; c->fresnel_pow = power;
+    return VRHIP_OK;
+}
+
+int vrhip_use_cornell_box(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->cornell = e != 0; return VRHIP_OK; }
+int vrhip_use_example_sphere(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->example = e != 0; return VRHIP_OK; }
+int vrhip_use_brdf(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->view_brdf = e != 0; return VRHIP_OK; }
+
+int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, const float* verts,
+                           const float* normals, const float* tangents, const float* uvs, size_t n_slots)
+{
+    if (!c || !bvh || !verts || !normals || !tangents || !uvs) return fail(VRHIP_ERR_INVALID, "null mesh array");
+    uint32_t depth = 0, nodes = 0;
+    int v = vr::validate_flat(bvh, n_bvh_f4, verts, n_slots, &depth, &nodes);
+    if (v != 0) return fail(VRHIP_ERR_BVH, "flattened BVH failed validation (code " + std::to_string(v) + ")");
+    if (depth > 62) return fail(VRHIP_ERR_BVH, "BVH deeper than 62 levels");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = upload(c, c->bvh, bvh, n_bvh_f4 * 16))) return rc;
+    if ((rc = upload(c, c->verts, verts, n_slots * 16))) return rc;
+    if ((rc = upload(c, c->normals, normals, n_slots * 16))) return rc;
+    if ((rc = upload(c, c->tangents, tangents, n_slots * 16))) return rc;
+    if ((rc = upload(c, c->uvs, uvs, n_slots * 8))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->n_bvh = n_bvh_f4; c->n_slots = n_slots;
+    c->bvh_depth = depth; c->bvh_nodes = nodes;
+    c->mesh = true;
+    return VRHIP_OK;
+}
+
+int vrhip_upload_mesh_indexed(vrhip_ctx* c, const float* positions, const float* normals, const float* tangents,
+                              const float* uvs, uint32_t n_verts, const uint32_t* tris, uint32_t n_tris,
+                              uint32_t max_leaf_tris)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    vr::FlatMesh m;
+    if (vr::build_flat(positions, normals, tangents, uvs, n_verts, tris, n_tris, max_leaf_tris, m) != 0)
+        return fail(VRHIP_ERR_INVALID, "BVH build failed (empty mesh or bad indices)");
+    return vrhip_upload_mesh_flat(c, (const float*)m.bvh.data(), m.bvh.size(), (const float*)m.verts.data(),
+                                  (const float*)m.normals.data(), (const float*)m.tangents.data(),
+                                  (const float*)m.uvs.data(), m.verts.size());
+}
+
+int vrhip_upload_hdr(vrhip_ctx* c, const float* rgba, uint32_t w, uint32_t h)
+{
+    if (!c || !rgba || w == 0 || h == 0) return fail(VRHIP_ERR_INVALID, "bad hdr arguments");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = upload(c, c->hdr, rgba, (size_t)w * h * 16))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->hdr_w = w; c->hdr_h = h;
+    return VRHIP_OK;
+}
+
+int vrhip_upload_hdr_half(vrhip_ctx* c, const uint16_t* rgba_half, uint32_t w, uint32_t h)
+{
+    if (!c || !rgba_half || w == 0 || h == 0) return fail(VRHIP_ERR_INVALID, "bad hdr arguments");
+    int rc = set_device(c); if (rc) return rc;
+    const size_t n = (size_t)w * h;
+    uint16_t* tmp = nullptr;
+    HIP_TRY(hipMalloc((void**)&tmp, n * 8));
+    dfree(c->hdr);
+    if (hipMalloc((void**)&c->hdr, n * 16) != hipSuccess) { dfree(tmp); return fail(VRHIP_ERR_NOMEM, "hdr alloc"); }
+    HIP_TRY(hipMemcpyAsync(tmp, rgba_half, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (vr::launch_half_to_float(tmp, c->hdr, n, c->stream) != 0) { dfree(tmp); return fail(VRHIP_ERR_HIP, "half convert"); }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    dfree(tmp);
+    c->hdr_w = w; c->hdr_h = h;
+    return VRHIP_OK;
+}
+
+int vrhip_upload_texture(vrhip_ctx* c, int type, const float* rgba, uint32_t w, uint32_t h)
+{
+    if (!c || !rgba || w == 0 || h == 0 || type < 0 || type > 2) return fail(VRHIP_ERR_INVALID, "bad texture arguments");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = upload(c, c->tex[type], rgba, (size_t)w * h * 16))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->tex_w[type] = w; c->tex_h[type] = h;
+    return VRHIP_OK;
+}
+
+int vrhip_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
+{
+    const size_t n = 90u * 90u * 360u / 2u;    // BRDF_SAMPLING_RES_* (include/vRenderer.h:23-25)
+    if (!c || !table || n_floats != 3 * n) return fail(VRHIP_ERR_INVALID, "BRDF table must hold 3*1458000 floats");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = upload(c, c->brdf, table, 3 * n * sizeof(float)))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return VRHIP_OK;
+}
+
+static int account_pending(vrhip_ctx* c)
+{
+    if (!c->pending) return VRHIP_OK;
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->kernel_ms_total += ms;
+    c->launches_total += c->launches_pending;
+    c->pending = false;
+    c->launches_pending = 0;
+    return VRHIP_OK;
+}
+
+static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed, bool count)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    if (n_frames == 0) return VRHIP_OK;
+    if (!c->cornell && !c->hdr)
+        return fail(VRHIP_ERR_NO_ENV, "HDRI mode needs an environment map (vrhip_upload_hdr)");
+    int rc = set_device(c); if (rc) return rc;
+    vr::RenderParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.cam_o = vr4{ c->cam_o[0], c->cam_o[1], c->cam_o[2], 0.f };
+    p.cam_d = vr4{ c->cam_d[0], c->cam_d[1], c->cam_d[2], 0.f };
+    // PathTracer.cu:833-836 in the same fp32 operation order
+    const float sx = c->fov_scale * (float)c->W / (float)c->H;
+    p.cx = vr4{ sx * c->cam_right[0], sx * c->cam_right[1], sx * c->cam_right[2], 0.f };
+    p.cy = vr4{ c->fov_scale * c->cam_up[0], c->fov_scale * c->cam_up[1], c->fov_scale * c->cam_up[2], 0.f };
+    p.W = c->W; p.H = c->H;
+    p.wr = (c->W / 16u) * 16u; p.hr = rendered_rows(c);
+    p.fresnel_coef = c->fresnel_coef; p.fresnel_pow = c->fresnel_pow;
+    uint32_t f = 0;
+    if (c->cornell) f |= vr::F_CORNELL;
+    if (c->example) f |= vr::F_EXAMPLE;
+    if (c->view_brdf) f |= vr::F_VIEW_BRDF;
+    if (c->mesh) f |= vr::F_MESH;
+    if (c->brdf) f |= vr::F_BRDF;
+    if (c->tex[0]) f |= vr::F_TEX_DIFF;
+    if (c->tex[1]) f |= vr::F_TEX_NORM;
+    if (c->tex[2]) f |= vr::F_TEX_SPEC;
+    p.flags = f;
+    p.tiles_x = p.wr / 16u;
+    p.rank = c->rank; p.nranks = c->nranks;
+    p.bvh = c->bvh; p.verts = c->verts; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
+    p.hdr = c->hdr; p.hdr_w = c->hdr_w; p.hdr_h = c->hdr_h;
+    for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
+    p.brdf = c->brdf;
+    p.accum = c->accum; p.rgba = c->rgba; p.depth = c->depth;
+    const uint32_t n_tiles = (owned_rows_of(c, c->rank) / 16u) * p.tiles_x;
+    const int stack = c->bvh_depth <= 30 ? 32 : 64;
+    if (count) {
+        if (!c->counters) HIP_TRY(hipMalloc((void**)&c->counters, sizeof(unsigned long long) * vr::kCounters));
+        HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
+        p.counters = c->counters;
+    }
+    if ((rc = account_pending(c)) != VRHIP_OK) return rc;
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    uint32_t done = 0;
+    while (done < n_frames) {
+        const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
+        p.first_frame = c->frame;
+        p.n_frames = k;
+        for (uint32_t i = 0; i < k; ++i) p.times[i] = times ? times[done + i] : time_seed;
+        int e = vr::launch_render(p, n_tiles, stack, count, c->stream);
+        if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
+        c->frame += k;
+        done += k;
+        c->launches_pending += n_tiles ? 1 : 0;
+    }
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    c->pending = true;
+    return VRHIP_OK;
+}
+
+int vrhip_render(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed)
+{
+    return render_impl(c, n_frames, times, time_seed, false);
+}
+
+int vrhip_render_counted(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed,
+                         uint64_t counters[8])
+{
+    if (!counters) return fail(VRHIP_ERR_INVALID, "counters is NULL");
+    int rc = render_impl(c, n_frames, times, time_seed, true);
+    if (rc) return rc;
+    unsigned long long h[vr::kCounters] = {};
+    HIP_TRY(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < vr::kCounters; ++i) counters[i] = (uint64_t)h[i];
+    return VRHIP_OK;
+}
+
+int vrhip_kernel_stats(vrhip_ctx* c, double* total_ms, uint64_t* launches, int reset)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = account_pending(c)) != VRHIP_OK) return rc;
+    if (total_ms) *total_ms = c->kernel_ms_total;
+    if (launches) *launches = c->launches_total;
+    if (reset) { c->kernel_ms_total = 0.0; c->launches_total = 0; }
+    return VRHIP_OK;
+}
+
+int vrhip_sync(vrhip_ctx* c)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    int rc = set_device(c); if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return VRHIP_OK;
+}
+
+int vrhip_frame_count(vrhip_ctx* c, uint32_t* frames)
+{
+    if (!c || !frames) return fail(VRHIP_ERR_INVALID, "null argument");
+    *frames = c->frame - 1;
+    return VRHIP_OK;
+}
+
+static int readback(vrhip_ctx* c, const void* src, void* dst, size_t bytes)
+{
+    if (!c || !dst) return fail(VRHIP_ERR_INVALID, "null argument");
+    int rc = set_device(c); if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return VRHIP_OK;
+}
+
+int vrhip_read_accum(vrhip_ctx* c, float* out) { return c ? readback(c, c->accum, out, (size_t)c->W * c->H * 16) : fail(VRHIP_ERR_INVALID, "null ctx"); }
+int vrhip_read_rgba8(vrhip_ctx* c, uint8_t* out) { return c ? readback(c, c->rgba, out, (size_t)c->W * c->H * 4) : fail(VRHIP_ERR_INVALID, "null ctx"); }
+int vrhip_read_depth8(vrhip_ctx* c, uint8_t* out) { return c ? readback(c, c->depth, out, (size_t)c->W * c->H * 4) : fail(VRHIP_ERR_INVALID, "null ctx"); }
+
+int vrhip_device_buffers(vrhip_ctx* c, void** accum, void** rgba8, void** depth8)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    if (accum) *accum = c->accum;
+    if (rgba8) *rgba8 = c->rgba;
+    if (depth8) *depth8 = c->depth;
+    return VRHIP_OK;
+}
+
+int vrhip_set_tiling(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks)
+{
+    if (!c || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad tiling");
+    c->rank = rank; c->nranks = n_ranks;
+    return VRHIP_OK;
+}
+
+int vrhip_owned_rows(vrhip_ctx* c, uint32_t* rows)
+{
+    if (!c || !rows) return fail(VRHIP_ERR_INVALID, "null argument");
+    *rows = owned_rows_of(c, c->rank);
+    return VRHIP_OK;
+}
+
+static int elem_size(int what) { return what == 1 ? 16 : 4; }
+static const void* buf_of(vrhip_ctx* c, int what) { return what == 1 ? (const void*)c->accum : what == 2 ? (const void*)c->depth : (const void*)c->rgba; }
+
+int vrhip_pack_rows(vrhip_ctx* c, int what, void* dst)
+{
+    if (!c || !dst || what < 0 || what > 2) return fail(VRHIP_ERR_INVALID, "bad pack arguments");
+    int rc = set_device(c); if (rc) return rc;
+    int e = vr::launch_pack_rows(buf_of(c, what), dst, (uint32_t)elem_size(what), c->W, rendered_rows(c),
+                                 c->rank, c->nranks, 0, c->stream);
+    if (e) return fail(VRHIP_ERR_HIP, "pack launch failed");
+    return VRHIP_OK;
+}
+
+int vrhip_unpack_rows(vrhip_ctx* c, int what, const void* src, uint32_t n_ranks, size_t stride_bytes)
+{
+    if (!c || !src || what < 0 || what > 2 || n_ranks == 0) return fail(VRHIP_ERR_INVALID, "bad unpack arguments");
+    int rc = set_device(c); if (rc) return rc;
+    const uint32_t saved_n = c->nranks;
+    c->nranks = n_ranks;
+    const char* s = (const char*)src;
+    for (uint32_t r = 0; r < n_ranks; ++r) {
+        int e = vr::launch_pack_rows(s, const_cast<void*>(buf_of(c, what)), (uint32_t)elem_size(what), c->W,
+                                     rendered_rows(c), r, n_ranks, 1, c->stream);
+        if (e) { c->nranks = saved_n; return fail(VRHIP_ERR_HIP, "unpack launch failed"); }
+        s += stride_bytes ? stride_bytes : (size_t)owned_rows_of(c, r) * c->W * elem_size(what);
+    }
+    c->nranks = saved_n;
+    return VRHIP_OK;
+}
+
+int vrhip_last_kernel_ms(vrhip_ctx* c, float* ms)
+{
+    if (!c || !ms) return fail(VRHIP_ERR_INVALID, "null argument");
+    if (!c->timed) { *ms = 0.f; return VRHIP_OK; }
+    HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return VRHIP_OK;
+}
+
+int vrhip_bvh_info(vrhip_ctx* c, uint32_t* depth, uint32_t* n_nodes, uint32_t* n_slots)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    if (depth) *depth = c->bvh_depth;
+    if (n_nodes) *n_nodes = c->bvh_nodes;
+    if (n_slots) *n_slots = (uint32_t)c->n_slots;
+    return VRHIP_OK;
+}
+
+int vrhip_selftest_math(int device, int fn, const float* a, const float* b, float* out, size_t n)
+{
+    if (!a || !b || !out) return fail(VRHIP_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(device));
+    float *da = nullptr, *db = nullptr, *dout = nullptr;
+    HIP_TRY(hipMalloc((void**)&da, n * 4 + 4));
+    HIP_TRY(hipMalloc((void**)&db, n * 4 + 4));
+    HIP_TRY(hipMalloc((void**)&dout, n * 4 + 4));
+    HIP_TRY(hipMemcpy(da, a, n * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(db, b, n * 4, hipMemcpyHostToDevice));
+    int e = vr::launch_selftest_math(fn, da, db, dout, n, nullptr);
+    if (e) return fail(VRHIP_ERR_HIP, "selftest launch failed");
+    HIP_TRY(hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout);
+    return VRHIP_OK;
+}
+
+int vrhip_build_flat(const float* positions, const float* normals, const float* tangents, const float* uvs,
+                     uint32_t n_verts, const uint32_t* tris, uint32_t n_tris, uint32_t max_leaf_tris,
+                     float* bvh_out, size_t* n_bvh_f4, float* verts_out, float* normals_out,
+                     float* tangents_out, float* uvs_out, size_t* n_slots)
+{
+    if (!n_bvh_f4 || !n_slots) return fail(VRHIP_ERR_INVALID, "size outputs are required");
+    vr::FlatMesh m;
+    if (vr::build_flat(positions, normals, tangents, uvs, n_verts, tris, n_tris, max_leaf_tris, m) != 0)
+        return fail(VRHIP_ERR_INVALID, "BVH build failed (empty mesh or bad indices)");
+    const bool fill = bvh_out && verts_out && normals_out && tangents_out && uvs_out;
+    if (fill) {
+        if (*n_bvh_f4 < m.bvh.size() || *n_slots < m.verts.size()) return fail(VRHIP_ERR_INVALID, "output arrays too small");
+        std::memcpy(bvh_out, m.bvh.data(), m.bvh.size() * 16);
+        std::memcpy(verts_out, m.verts.data(), m.verts.size() * 16);
+        std::memcpy(normals_out, m.normals.data(), m.normals.size() * 16);
+        std::memcpy(tangents_out, m.tangents.data(), m.tangents.size() * 16);
+        std::memcpy(uvs_out, m.uvs.data(), m.uvs.size() * 8);
+    }
+    *n_bvh_f4 = m.bvh.size();
+    *n_slots = m.verts.size();
+    return VRHIP_OK;
+}
+
+int vrhip_validate_flat(const float* bvh, size_t n_bvh_f4, const float* verts, size_t n_slots,
+                        uint32_t* depth, uint32_t* n_nodes)
+{
+    int v = vr::validate_flat(bvh, n_bvh_f4, verts, n_slots, depth, n_nodes);
+    if (v != 0) return fail(VRHIP_ERR_BVH, "validation failed (code " + std::to_string(v) + ")");
+    return VRHIP_OK;
+}
+
+} // extern "C"

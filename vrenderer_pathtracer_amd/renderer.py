@@ -1,0 +1,352 @@
+"""Python host mirror of the reference's renderer interface, over the C ABI.
+
+`VRendererHIP` has the method names, argument meanings and error behaviour of
+the reference's abstract `vRenderer` (include/vRenderer.h:30-168) as
+implemented by `vRendererCuda` (src/vRendererCuda.cpp), so tests read like
+code driving the reference.  Differences, all deliberate:
+  * errors raise VRHIPError instead of printing, writing errorlog.txt and
+    calling exit(0) (src/vRendererCuda.cpp:454-467);
+  * GL interop (registerTextureBuffer / registerDepthBuffer) is replaced by
+    device RGBA8 buffers plus read-back (headless);
+  * render(frames=K) renders K progressive frames in one device pass;
+  * the RNG `_time` seed is explicit (the reference uses wall-clock ms,
+    src/vRendererCuda.cpp:114,153).
+"""
+from __future__ import annotations
+
+import ctypes
+import time as _time
+
+import numpy as np
+
+from . import _native
+from ._native import VRHIPError, check, fptr
+
+BRDF_SAMPLING_RES_THETA_H = 90      # include/vRenderer.h:23-25
+BRDF_SAMPLING_RES_THETA_D = 90
+BRDF_SAMPLING_RES_PHI_D = 360
+BRDF_TABLE_FLOATS = 3 * BRDF_SAMPLING_RES_THETA_H * BRDF_SAMPLING_RES_THETA_D * BRDF_SAMPLING_RES_PHI_D // 2
+
+DIFFUSE, NORMAL, SPECULAR = 0, 1, 2     # vTextureType (cuda/include/PathTracer.cuh:86)
+
+
+def _f32(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+def build_flat(mesh: dict, max_leaf_tris: int = 4) -> dict:
+    """Native BVH build + reference flattening (src/vRendererCuda.cpp:204-279).
+
+    mesh: positions (N,3), normals (N,3), tangents (N,3), uvs (N,2), tris (M,3) uint32.
+    Returns dict bvh (n,4), verts/normals/tangents (s,4), uvs (s,2) float32 arrays.
+    """
+    L = _native.lib()
+    pos = _f32(mesh["positions"])
+    nrm = _f32(mesh["normals"]) if mesh.get("normals") is not None else None
+    tan = _f32(mesh["tangents"]) if mesh.get("tangents") is not None else None
+    uvs = _f32(mesh["uvs"]) if mesh.get("uvs") is not None else None
+    tris = np.ascontiguousarray(mesh["tris"], dtype=np.uint32)
+    nv, nt = pos.shape[0], tris.shape[0]
+    n_bvh = ctypes.c_size_t(0)
+    n_slots = ctypes.c_size_t(0)
+    tp = tris.ctypes.data_as(_native._u32)
+    check(L.vrhip_build_flat(fptr(pos), fptr(nrm), fptr(tan), fptr(uvs), nv, tp, nt, max_leaf_tris,
+                             None, ctypes.byref(n_bvh), None, None, None, None, ctypes.byref(n_slots)),
+          "vrhip_build_flat(size)")
+    out = {"bvh": np.zeros((n_bvh.value, 4), np.float32),
+           "verts": np.zeros((n_slots.value, 4), np.float32),
+           "normals": np.zeros((n_slots.value, 4), np.float32),
+           "tangents": np.zeros((n_slots.value, 4), np.float32),
+           "uvs": np.zeros((n_slots.value, 2), np.float32)}
+    check(L.vrhip_build_flat(fptr(pos), fptr(nrm), fptr(tan), fptr(uvs), nv, tp, nt, max_leaf_tris,
+                             fptr(out["bvh"]), ctypes.byref(n_bvh), fptr(out["verts"]), fptr(out["normals"]),
+                             fptr(out["tangents"]), fptr(out["uvs"]), ctypes.byref(n_slots)),
+          "vrhip_build_flat")
+    return out
+
+
+def validate_flat(flat: dict) -> tuple[int, int]:
+    """Returns (depth, inner node count) of a flattened tree, raising if malformed."""
+    L = _native.lib()
+    d = ctypes.c_uint32(0)
+    n = ctypes.c_uint32(0)
+    bvh = _f32(flat["bvh"])
+    verts = _f32(flat["verts"])
+    check(L.vrhip_validate_flat(fptr(bvh), bvh.size // 4, fptr(verts), verts.size // 4, ctypes.byref(d),
+                                ctypes.byref(n)), "vrhip_validate_flat")
+    return d.value, n.value
+
+
+class Camera:
+    """Host camera state, the reference's Camera (src/Camera.cpp) reduced to
+    what the renderer consumes: origin, dir, up, right, fovScale."""
+
+    def __init__(self, origin=(0.0, 0.0, 150.0), dir=(0.0, 0.0, -1.0), up=(0.0, 1.0, 0.0),
+                 right=(1.0, 0.0, 0.0), fov_scale=None):
+        self.origin = np.asarray(origin, np.float32)
+        self.dir = np.asarray(dir, np.float32)
+        self.up = np.asarray(up, np.float32)
+        self.right = np.asarray(right, np.float32)
+        self.fov_scale = np.float32(default_fov_scale() if fov_scale is None else fov_scale)
+        self.dirty = False
+
+    def is_dirty(self) -> bool:
+        return self.dirty
+
+
+def default_fov_scale() -> float:
+    """Camera::getFovScale for the default 75 degree FOV (src/Camera.cpp:4,119-123), in fp32 + tanf."""
+    libm = ctypes.CDLL("libm.so.6")
+    libm.tanf.restype = ctypes.c_float
+    libm.tanf.argtypes = [ctypes.c_float]
+    k_deg_in_rad = np.float32(np.pi / np.float64(np.float32(180.0)))
+    fov_rad = np.float32(np.float32(75.0) * k_deg_in_rad)
+    return float(libm.tanf(float(np.float32(fov_rad / np.float32(2.0)))))
+
+
+class VRendererHIP:
+    """MI355X peer of vRendererCuda behind the vRenderer interface."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _native.lib()
+        self._ctx = ctypes.c_void_p(None)
+        self._device = device
+        self._camera = None
+        self.m_fresnelCoef = 0.1     # src/vRendererCuda.cpp:27-28
+        self.m_fresnelPow = 3.0
+        self.width = self.height = 0
+        self.default_time = None
+
+    # -- vRenderer pure virtuals (include/vRenderer.h:48-133) ------------
+    def init(self, w: int, h: int) -> None:
+        assert w != 0 and h != 0
+        if self._ctx:
+            self.cleanUp()
+        check(self._lib.vrhip_create(self._device, w, h, ctypes.byref(self._ctx)), "vrhip_create")
+        self.width, self.height = w, h
+        check(self._lib.vrhip_set_fresnel(self._ctx, self.m_fresnelCoef, self.m_fresnelPow), "vrhip_set_fresnel")
+
+    def registerTextureBuffer(self, texture=None) -> None:
+        """GL interop is replaced by the device RGBA8 buffer (read with read_rgba8)."""
+
+    def registerDepthBuffer(self, depth_texture=None) -> None:
+        """GL interop is replaced by the device depth buffer (read with read_depth8)."""
+
+    def render(self, frames: int = 1, times=None, time_seed=None, sync: bool = True) -> None:
+        self._need_ctx()
+        if self._camera is not None and self._camera.is_dirty():
+            self.updateCamera()
+        arr = None
+        if times is not None:
+            arr = (ctypes.c_uint32 * frames)(*[int(t) & 0xFFFFFFFF for t in times])
+        if time_seed is None:
+            time_seed = self.default_time if self.default_time is not None else int(_time.time() * 1000)
+        check(self._lib.vrhip_render(self._ctx, frames, arr, int(time_seed) & 0xFFFFFFFF), "vrhip_render")
+        if sync:
+            check(self._lib.vrhip_sync(self._ctx), "vrhip_sync")
+
+    def cleanUp(self) -> None:
+        if self._ctx:
+            self._lib.vrhip_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p(None)
+
+    def updateCamera(self) -> None:
+        self._need_ctx()
+        cam = self._camera or Camera()
+        check(self._lib.vrhip_set_camera(self._ctx, fptr(_f32(cam.origin)), fptr(_f32(cam.dir)),
+                                         fptr(_f32(cam.up)), fptr(_f32(cam.right)), float(cam.fov_scale)),
+              "vrhip_set_camera")
+        cam.dirty = False
+
+    def initMesh(self, mesh: dict) -> None:
+        """mesh: either a flattened dict (bvh/verts/normals/tangents/uvs, the
+        layout vRendererCuda::initMesh produces) or an indexed triangle mesh
+        (positions/normals/tangents/uvs/tris) that is built here."""
+        self._need_ctx()
+        flat = mesh if "bvh" in mesh else build_flat(mesh)
+        arrs = {k: _f32(flat[k]) for k in ("bvh", "verts", "normals", "tangents", "uvs")}
+        check(self._lib.vrhip_upload_mesh_flat(self._ctx, fptr(arrs["bvh"]), arrs["bvh"].size // 4,
+                                               fptr(arrs["verts"]), fptr(arrs["normals"]),
+                                               fptr(arrs["tangents"]), fptr(arrs["uvs"]),
+                                               arrs["verts"].size // 4), "vrhip_upload_mesh_flat")
+
+    def loadHDR(self, pixels, w: int = None, h: int = None) -> None:
+        """pixels: float32 (H,W,4) or float16 (H,W,4) (Imf::Rgba layout)."""
+        self._need_ctx()
+        a = np.ascontiguousarray(pixels)
+        h = a.shape[0] if h is None else h
+        w = a.shape[1] if w is None else w
+        if a.dtype == np.float16:
+            check(self._lib.vrhip_upload_hdr_half(self._ctx, a.view(np.uint16).ctypes.data_as(_native._u16), w, h),
+                  "vrhip_upload_hdr_half")
+        else:
+            a = _f32(a)
+            check(self._lib.vrhip_upload_hdr(self._ctx, fptr(a), w, h), "vrhip_upload_hdr")
+
+    def loadTexture(self, texture, gamma: float = 1.0, type: int = DIFFUSE) -> None:
+        """texture: uint8 (H,W,4) image (QImage pixels) -> float4 as
+        vRendererCuda::loadTexture does (inverse gamma on DIFFUSE only,
+        src/vRendererCuda.cpp:344-368); or a float32 (H,W,4) array used as is."""
+        self._need_ctx()
+        t = np.asarray(texture)
+        if t.dtype == np.uint8:
+            c = np.float32(1.0 / gamma) if gamma > 0.001 else np.float32(1.0)
+            f = t.astype(np.float32) / np.float32(255.0)
+            if type == DIFFUSE:
+                f[..., :3] = np.power(f[..., :3], c, dtype=np.float32)
+            t = f
+        t = _f32(t)
+        check(self._lib.vrhip_upload_texture(self._ctx, int(type), fptr(t), t.shape[1], t.shape[0]),
+              "vrhip_upload_texture")
+
+    def useBRDF(self, v: bool) -> None:
+        self._need_ctx()
+        check(self._lib.vrhip_use_brdf(self._ctx, int(bool(v))), "vrhip_use_brdf")
+
+    def useExampleSphere(self, v: bool) -> None:
+        self._need_ctx()
+        check(self._lib.vrhip_use_example_sphere(self._ctx, int(bool(v))), "vrhip_use_example_sphere")
+
+    def useCornellBox(self, v: bool) -> None:
+        self._need_ctx()
+        check(self._lib.vrhip_use_cornell_box(self._ctx, int(bool(v))), "vrhip_use_cornell_box")
+
+    def clearBuffer(self) -> None:
+        self._need_ctx()
+        check(self._lib.vrhip_clear(self._ctx), "vrhip_clear")
+
+    def loadBRDF(self, brdf) -> bool:
+        """Returns False for None, like vRendererCuda::loadBRDF (src/vRendererCuda.cpp:413-437)."""
+        if brdf is None:
+            return False
+        self._need_ctx()
+        b = _f32(brdf).reshape(-1)
+        check(self._lib.vrhip_upload_brdf(self._ctx, fptr(b), b.size), "vrhip_upload_brdf")
+        return True
+
+    def getFrameCount(self) -> int:
+        self._need_ctx()
+        n = ctypes.c_uint32(0)
+        check(self._lib.vrhip_frame_count(self._ctx, ctypes.byref(n)), "vrhip_frame_count")
+        return n.value
+
+    # -- non-virtual vRenderer members (include/vRenderer.h:139-151) -----
+    def setFresnelCoef(self, v: float) -> None:
+        self.m_fresnelCoef = float(v)
+        self._need_ctx()
+        check(self._lib.vrhip_set_fresnel(self._ctx, self.m_fresnelCoef, self.m_fresnelPow), "vrhip_set_fresnel")
+        self.clearBuffer()
+
+    def setFresnelPower(self, v: float) -> None:
+        self.m_fresnelPow = float(v)
+        self._need_ctx()
+        check(self._lib.vrhip_set_fresnel(self._ctx, self.m_fresnelCoef, self.m_fresnelPow), "vrhip_set_fresnel")
+        self.clearBuffer()
+
+    def setCamera(self, cam: Camera) -> None:
+        self._camera = cam
+        self.updateCamera()
+
+    # -- read-back / multi-GPU helpers ------------------------------------
+    def read_accum(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), np.float32)
+        check(self._lib.vrhip_read_accum(self._need_ctx(), fptr(out)), "vrhip_read_accum")
+        return out
+
+    def read_rgba8(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), np.uint8)
+        check(self._lib.vrhip_read_rgba8(self._need_ctx(), out.ctypes.data_as(_native._u8)), "vrhip_read_rgba8")
+        return out
+
+    def read_depth8(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), np.uint8)
+        check(self._lib.vrhip_read_depth8(self._need_ctx(), out.ctypes.data_as(_native._u8)), "vrhip_read_depth8")
+        return out
+
+    def set_stream(self, stream_handle) -> None:
+        check(self._lib.vrhip_set_stream(self._need_ctx(), ctypes.c_void_p(stream_handle)), "vrhip_set_stream")
+
+    def sync(self) -> None:
+        check(self._lib.vrhip_sync(self._need_ctx()), "vrhip_sync")
+
+    def set_tiling(self, rank: int, n_ranks: int) -> None:
+        check(self._lib.vrhip_set_tiling(self._need_ctx(), rank, n_ranks), "vrhip_set_tiling")
+
+    def owned_rows(self) -> int:
+        n = ctypes.c_uint32(0)
+        check(self._lib.vrhip_owned_rows(self._need_ctx(), ctypes.byref(n)), "vrhip_owned_rows")
+        return n.value
+
+    def pack_rows(self, what: int, dst_ptr: int) -> None:
+        check(self._lib.vrhip_pack_rows(self._need_ctx(), what, ctypes.c_void_p(dst_ptr)), "vrhip_pack_rows")
+
+    def unpack_rows(self, what: int, src_ptr: int, n_ranks: int, stride_bytes: int = 0) -> None:
+        check(self._lib.vrhip_unpack_rows(self._need_ctx(), what, ctypes.c_void_p(src_ptr), n_ranks, stride_bytes),
+              "vrhip_unpack_rows")
+
+    def render_counted(self, frames: int = 1, times=None, time_seed=None) -> dict:
+        """Render through the counting kernel variant; returns the event counts."""
+        arr = None
+        if times is not None:
+            arr = (ctypes.c_uint32 * frames)(*[int(t) & 0xFFFFFFFF for t in times])
+        if time_seed is None:
+            time_seed = self.default_time if self.default_time is not None else int(_time.time() * 1000)
+        c = (ctypes.c_uint64 * 8)()
+        check(self._lib.vrhip_render_counted(self._need_ctx(), frames, arr, int(time_seed) & 0xFFFFFFFF, c),
+              "vrhip_render_counted")
+        names = ["rays", "node_visits", "slot_reads", "tri_tests", "attr_bytes", "tex_fetches", "hdr_fetches",
+                 "brdf_fetches"]
+        return {n: int(v) for n, v in zip(names, c)}
+
+    def kernel_stats(self, reset: bool = False):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_uint64(0)
+        check(self._lib.vrhip_kernel_stats(self._need_ctx(), ctypes.byref(ms), ctypes.byref(n), int(reset)),
+              "vrhip_kernel_stats")
+        return float(ms.value), int(n.value)
+
+    def device_buffers(self):
+        a, r, d = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        check(self._lib.vrhip_device_buffers(self._need_ctx(), ctypes.byref(a), ctypes.byref(r), ctypes.byref(d)),
+              "vrhip_device_buffers")
+        return a.value, r.value, d.value
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_float(0)
+        check(self._lib.vrhip_last_kernel_ms(self._need_ctx(), ctypes.byref(ms)), "vrhip_last_kernel_ms")
+        return float(ms.value)
+
+    def bvh_info(self):
+        d, n, s = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        check(self._lib.vrhip_bvh_info(self._need_ctx(), ctypes.byref(d), ctypes.byref(n), ctypes.byref(s)),
+              "vrhip_bvh_info")
+        return d.value, n.value, s.value
+
+    def _need_ctx(self):
+        if not self._ctx:
+            raise VRHIPError(-1, "VRendererHIP", "init() has not been called")
+        return self._ctx
+
+    def __del__(self):
+        try:
+            self.cleanUp()
+        except Exception:
+            pass
+
+
+def selftest_math(fn: int, a, b=None, device: int = 0) -> np.ndarray:
+    """Evaluate the device libm (0 sin, 1 cos, 2 acos, 3 atan2, 4 pow, 5 fmin, 6 fmax, 7 f2i)."""
+    a = _f32(a).reshape(-1)
+    b = _f32(np.zeros_like(a) if b is None else b).reshape(-1)
+    out = np.zeros_like(a)
+    check(_native.lib().vrhip_selftest_math(device, fn, fptr(a), fptr(b), fptr(out), a.size), "vrhip_selftest_math")
+    return out
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = _native.lib().vrhip_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
