@@ -39,10 +39,11 @@ PROFILE_TRAFFIC = os.path.join(REPO, "profiles", "traffic_c2.json")
 
 
 def algorithmic_bytes(c: dict, paths: int, pixel_frames: int) -> float:
-    """64 B/node visit, 16 B/vert0 slot read, +32 B/triangle
-    tested, hit attribute bytes, 16 B/texture or HDRI fetch, 12 B/BRDF lookup,
+    """SURVEY.md 8d byte costs, as the kernel executes them: 64 B/node visit,
+    48 B/triangle tested (16 B per terminator slot read, 0 with the device
+    layout), hit attribute bytes, 16 B/texture or HDRI fetch, 12 B/BRDF lookup,
     92 B of pixel I/O per pixel-frame."""
-    return (64 * c["node_visits"] + 16 * c["slot_reads"] + 32 * c["tri_tests"] + c["attr_bytes"]
+    return (64 * c["node_visits"] + 16 * c["slot_reads"] + 48 * c["tri_tests"] + c["attr_bytes"]
             + 16 * c["tex_fetches"] + 16 * c["hdr_fetches"] + 12 * c["brdf_fetches"] + 92 * pixel_frames)
 
 
@@ -53,17 +54,22 @@ def cpu_baseline(scene: dict, budget_s: float, threads: int) -> dict:
     pyoracle.build()
     W, H = scene["width"], scene["height"]
     accum = np.zeros((H, W, 4), np.float32)
-    rows, t0 = 0, time.perf_counter()
+    paths, frames, t0 = 0, 0, time.perf_counter()
     chunk = 16
-    while rows < H and time.perf_counter() - t0 < budget_s:
-        r1 = min(H, rows + chunk)
-        pyoracle.render(scene, frames=1, times=[scene["time"]], rows=(rows, r1), threads=threads, accum=accum)
-        rows = r1
+    while time.perf_counter() - t0 < budget_s and frames < 64:
+        frame = frames + 1
+        for r0 in range(0, H, chunk):
+            pyoracle.render(scene, frames=1, times=[scene["time"] + frames], first_frame=frame,
+                            rows=(r0, min(H, r0 + chunk)), threads=threads, accum=accum)
+            paths += (min(H, r0 + chunk) - r0) * W * 2
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        frames += 1
     dt = time.perf_counter() - t0
-    paths = rows * W * 2
+    rows = paths // (2 * W)
     return {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ C restatement (glibc libm, -O2, OpenMP {threads} threads), frame 1 of C2 "
-                      f"1280x720, rows 0-{rows - 1} ({paths} paths, {dt:.1f} s)"}
+            "sample": f"oracle/ C restatement (glibc libm, -O2, OpenMP {threads} threads), C2 "
+                      f"1280x720, {rows} rows over {frames} frame(s) ({paths} paths, {dt:.1f} s)"}
 
 
 def main():

@@ -71,6 +71,13 @@ int vrhip_set_fresnel(vrhip_ctx *ctx, float coef, float power);
 int vrhip_use_cornell_box(vrhip_ctx *ctx, int enable);
 int vrhip_use_example_sphere(vrhip_ctx *ctx, int enable);
 int vrhip_use_brdf(vrhip_ctx *ctx, int enable);
+/* Traversal mode.  Default (0): children whose slab entry lies beyond the
+ * closest hit so far (x 1.0009765625) are skipped -- the reference visits
+ * every box the ray's line pierces (span end clamped to 1e20,
+ * cuda/src/PathTracer.cu:316,322); skipping them leaves the closest hit
+ * unchanged except in fp32 rounding corner cases.  1: visit
+ * every pierced box exactly as the reference. */
+int vrhip_set_strict_traversal(vrhip_ctx *ctx, int enable);
 
 /* ---- scene uploads ---------------------------------------------------- */
 /* replaces the device half of vRendererCuda::initMesh
@@ -117,7 +124,8 @@ int vrhip_render(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint3
 /* Same render, through the counting kernel variant (identical results, plus
  * per-event counts for the roofline's algorithmic bytes):
  * counters[0..7] = rays (intersectScene calls), inner-node visits (64 B),
- * vert0 slot reads incl. terminators (16 B), triangle tests (+32 B), hit
+ * terminator slot reads (16 B; 0 with the device layout), triangle tests
+ * (48 B), hit
  * attribute bytes, texture fetches (16 B), HDRI fetches (16 B), BRDF lookups
  * (12 B).  Synchronous. */
 int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,

@@ -44,6 +44,7 @@ _SIGNATURES = {
     "vrhip_use_cornell_box": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "vrhip_use_example_sphere": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "vrhip_use_brdf": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "vrhip_set_strict_traversal": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "vrhip_upload_mesh_flat": (ctypes.c_int, [_ctx, _f, ctypes.c_size_t, _f, _f, _f, _f, ctypes.c_size_t]),
     "vrhip_upload_mesh_indexed": (ctypes.c_int, [_ctx, _f, _f, _f, _f, ctypes.c_uint32, _u32, ctypes.c_uint32,
                                                  ctypes.c_uint32]),

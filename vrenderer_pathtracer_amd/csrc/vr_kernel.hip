@@ -127,6 +127,17 @@ __device__ __forceinline__ vr4 sphere_normal(const HitRec& hr, const Ray& r) {
     return normalize4(sub4(hp, mk4(s.px, s.py, s.pz, 0.f)));
 }
 
+// Device mesh layout (built from the reference layout at upload, vrhip_api.cpp):
+//   nodes: the reference's 4 x float4 per inner node, except that a leaf
+//          child is ~((first_tri << 7) | tri_count) into the compact arrays;
+//   tris:  3 float4 vertex positions per triangle, leaves contiguous, in the
+//          reference's slot order (no terminator slots);
+//   attributes (normals, tangents, uvs): same indexing, fetched only for the
+//          final hit of a ray.
+// The triangles tested and their order are those of the reference layout, so
+// the closest hit (ties included) is unchanged.
+constexpr int kLeafCountBits = 7;
+
 template <int STACK, bool COUNT>
 __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, int* stk, Cnt& cnt)
 {
@@ -141,6 +152,13 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
     const float ivz = 1.f / (__builtin_fabsf(r.d.z) > VR_EPS ? r.d.z : VR_EPS);
     const float odx = r.o.x * ivx, ody = r.o.y * ivy, odz = r.o.z * ivz;
     float t = hr.t;
+    // t-culling: a child whose slab entry lies beyond the closest hit so far
+    // (times a 2^-10 safety margin) cannot hold a closer triangle.  The
+    // reference visits every pierced box (span end clamped to 1e20,
+    // :316,322); F_STRICT restores that exactly.
+    const bool strict = (p.flags & F_STRICT) != 0;
+    const float kCull = 1.0009765625f;
+    float tcull = strict ? __builtin_inff() : t * kCull;
     int best = -1;
     float bu = 0.f, bv = 0.f;
 
@@ -168,9 +186,11 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
             const float c1hiy = n1.w * ivy - ody;
             const float c1min = span_begin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 0.0f);
             const float c1max = span_end(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 1e20f);
+            // keep the child-index load in the same round trip as the bounds
+            asm volatile("" ::"v"(idx0), "v"(idx1));
             const bool swp = (c1min < c0min);
-            const bool tc0 = (c0max >= c0min);
-            const bool tc1 = (c1max >= c1min);
+            const bool tc0 = (c0max >= c0min) && (c0min <= tcull);
+            const bool tc1 = (c1max >= c1min) && (c1min <= tcull);
             if (!tc0 && !tc1) {
                 nodeAddr = stk[sp * kBlockThreads];
                 --sp;
@@ -190,11 +210,12 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
             if (__ballot(leafAddr >= 0) == 0ull) break;          // every lane holds a leaf
         }
         while (leafAddr < 0) {
-            for (int triAddr = ~leafAddr;; triAddr += 3) {
-                const vr4 v0 = p.verts[triAddr];
-                if (COUNT) cnt.slots++;
-                if (__float_as_uint(v0.x) == 0x80000000u) break;
+            const int lv = ~leafAddr;
+            const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
+            for (int k = lv >> kLeafCountBits; k < kend; ++k) {
+                const int triAddr = 3 * k;
                 if (COUNT) cnt.tris++;
+                const vr4 v0 = p.verts[triAddr];
                 const vr4 v1 = p.verts[triAddr + 1];
                 const vr4 v2 = p.verts[triAddr + 2];
                 // intersectTriangle, RayIntersection.cuh:54-111
@@ -210,7 +231,10 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
                 const float v = dot4(r.d, q) * inv_det;
                 if (v < 0.f || u + v > 1.f) continue;
                 const float dist = dot4(e2, q) * inv_det;
-                if (dist > VR_EPS && dist < t) { t = dist; best = triAddr; bu = u; bv = v; }
+                if (dist > VR_EPS && dist < t) {
+                    t = dist; best = triAddr; bu = u; bv = v;
+                    tcull = strict ? tcull : t * kCull;
+                }
             }
             leafAddr = nodeAddr;
             if (nodeAddr < 0) {

@@ -20,6 +20,7 @@ enum Flags : uint32_t {
     F_TEX_DIFF = 1u << 5,    // kHasDiffuseMap      (:25)
     F_TEX_NORM = 1u << 6,    // kHasNormalMap       (:26)
     F_TEX_SPEC = 1u << 7,    // kHasSpecularMap     (:27)
+    F_STRICT = 1u << 8,      // visit every pierced box, as the reference (no t-culling)
 };
 
 constexpr int kMaxFramesPerLaunch = 64;

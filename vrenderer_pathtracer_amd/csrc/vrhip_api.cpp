@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/vrhip.h"
@@ -54,6 +55,7 @@ struct vrhip_ctx {
     uint32_t frame = 1;                         // m_frame (src/vRendererCuda.cpp:24)
     float fresnel_coef = 0.1f, fresnel_pow = 3.f; // src/vRendererCuda.cpp:27-28
     bool cornell = false, example = false, view_brdf = false;
+    bool strict = false;          // exact reference traversal (no t-culling)
     // mesh
     vr4* bvh = nullptr; vr4* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
@@ -100,6 +102,67 @@ uint32_t owned_rows_of(const vrhip_ctx* c, uint32_t rank)
     const uint32_t bands = c->H / 16u;
     const uint32_t owned = bands > rank ? (bands - rank + c->nranks - 1) / c->nranks : 0;
     return owned * 16u;
+}
+
+// Device mesh layout (see vr_kernel.hip): the reference nodes with leaf
+// children re-encoded as ~((first_tri << 7) | count) into compact per-triangle
+// arrays (3 slots per triangle, terminator slots dropped).  Built from the
+// reference flattening (src/vRendererCuda.cpp:204-279) so the triangles a
+// leaf tests, and their order, are exactly the reference's.
+struct DeviceMesh {
+    std::vector<vr4> nodes, tris, normals, tangents;
+    std::vector<vr2> uvs;
+};
+
+constexpr int kLeafCountBits = 7;
+
+bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const vr4* normals,
+                      const vr4* tangents, const vr2* uvs, DeviceMesh& dm, std::string& why)
+{
+    dm.nodes.assign((const vr4*)bvh, (const vr4*)bvh + n_bvh_f4);
+    std::unordered_map<int32_t, int32_t> leaf_code;
+    std::vector<size_t> st{ 0 };
+    std::vector<uint8_t> seen(n_bvh_f4 / 4, 0);
+    while (!st.empty()) {
+        const size_t off = st.back();
+        st.pop_back();
+        if (seen[off / 4]) continue;
+        seen[off / 4] = 1;
+        float* idxf = &dm.nodes[off + 3].x;
+        for (int ch = 0; ch < 2; ++ch) {
+            int32_t idx;
+            std::memcpy(&idx, &idxf[ch], 4);
+            if (idx >= 0) { st.push_back((size_t)idx); continue; }
+            auto it = leaf_code.find(idx);
+            int32_t code;
+            if (it != leaf_code.end()) {
+                code = it->second;
+            } else {
+                const size_t first = dm.tris.size() / 3;
+                size_t s = (size_t)(~idx), count = 0;
+                for (;;) {
+                    uint32_t b;
+                    std::memcpy(&b, &verts[s].x, 4);
+                    if (b == 0x80000000u) break;
+                    for (int k = 0; k < 3; ++k) {
+                        dm.tris.push_back(verts[s + k]);
+                        dm.normals.push_back(normals[s + k]);
+                        dm.tangents.push_back(tangents[s + k]);
+                        dm.uvs.push_back(uvs[s + k]);
+                    }
+                    s += 3;
+                    ++count;
+                }
+                if (count >= (1u << kLeafCountBits)) { why = "leaf with >= 128 triangles"; return false; }
+                if (first >= (1u << (31 - kLeafCountBits))) { why = "more than 16M triangle references"; return false; }
+                code = ~(int32_t)((first << kLeafCountBits) | count);
+                leaf_code.emplace(idx, code);
+            }
+            std::memcpy(&idxf[ch], &code, 4);
+        }
+    }
+    if (dm.tris.empty()) { dm.tris.push_back(vr4{ 0, 0, 0, 0 }); dm.normals = dm.tangents = dm.tris; dm.uvs.push_back(vr2{ 0, 0 }); }
+    return true;
 }
 
 template <typename T>
@@ -213,6 +276,7 @@ int vrhip_set_fresnel(vrhip_ctx* c, float coef, float power)
 
 int vrhip_use_cornell_box(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->cornell = e != 0; return VRHIP_OK; }
 int vrhip_use_example_sphere(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->example = e != 0; return VRHIP_OK; }
+int vrhip_set_strict_traversal(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->strict = e != 0; return VRHIP_OK; }
 int vrhip_use_brdf(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->view_brdf = e != 0; return VRHIP_OK; }
 
 int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, const float* verts,
@@ -223,12 +287,18 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     int v = vr::validate_flat(bvh, n_bvh_f4, verts, n_slots, &depth, &nodes);
     if (v != 0) return fail(VRHIP_ERR_BVH, "flattened BVH failed validation (code " + std::to_string(v) + ")");
     if (depth > 62) return fail(VRHIP_ERR_BVH, "BVH deeper than 62 levels");
+    DeviceMesh dm;
+    std::string why;
+    if (!to_device_layout(bvh, n_bvh_f4, (const vr4*)verts, (const vr4*)normals, (const vr4*)tangents,
+                          (const vr2*)uvs, dm, why))
+        return fail(VRHIP_ERR_BVH, why);
     int rc = set_device(c); if (rc) return rc;
-    if ((rc = upload(c, c->bvh, bvh, n_bvh_f4 * 16))) return rc;
-    if ((rc = upload(c, c->verts, verts, n_slots * 16))) return rc;
-    if ((rc = upload(c, c->normals, normals, n_slots * 16))) return rc;
-    if ((rc = upload(c, c->tangents, tangents, n_slots * 16))) return rc;
-    if ((rc = upload(c, c->uvs, uvs, n_slots * 8))) return rc;
+    const size_t nt = dm.tris.size();
+    if ((rc = upload(c, c->bvh, dm.nodes.data(), dm.nodes.size() * 16))) return rc;
+    if ((rc = upload(c, c->verts, dm.tris.data(), nt * 16))) return rc;
+    if ((rc = upload(c, c->normals, dm.normals.data(), nt * 16))) return rc;
+    if ((rc = upload(c, c->tangents, dm.tangents.data(), nt * 16))) return rc;
+    if ((rc = upload(c, c->uvs, dm.uvs.data(), nt * 8))) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_bvh = n_bvh_f4; c->n_slots = n_slots;
     c->bvh_depth = depth; c->bvh_nodes = nodes;
@@ -331,6 +401,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     if (c->cornell) f |= vr::F_CORNELL;
     if (c->example) f |= vr::F_EXAMPLE;
     if (c->view_brdf) f |= vr::F_VIEW_BRDF;
+    if (c->strict) f |= vr::F_STRICT;
     if (c->mesh) f |= vr::F_MESH;
     if (c->brdf) f |= vr::F_BRDF;
     if (c->tex[0]) f |= vr::F_TEX_DIFF;

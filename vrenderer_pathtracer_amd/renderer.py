@@ -214,6 +214,10 @@ class VRendererHIP:
         self._need_ctx()
         check(self._lib.vrhip_use_cornell_box(self._ctx, int(bool(v))), "vrhip_use_cornell_box")
 
+    def set_strict_traversal(self, strict: bool) -> None:
+        """True: visit every box the ray pierces, exactly like the reference."""
+        check(self._lib.vrhip_set_strict_traversal(self._need_ctx(), int(bool(strict))), "vrhip_set_strict_traversal")
+
     def clearBuffer(self) -> None:
         self._need_ctx()
         check(self._lib.vrhip_clear(self._ctx), "vrhip_clear")
