@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""A/B timing of libvrhip.so build variants on one GPU (each in its own process).
+
+  python scripts/ab.py [--cfg C2] [--frames 8] [--steps 4] lib1.so lib2.so ...
+
+Prints Mpaths/s per variant (median of steps) and checks every variant's
+accumulation buffer bit-equals the first one's.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys, time, json, numpy as np
+sys.path.insert(0, {repo!r})
+import torch
+from vrenderer_pathtracer_amd import VRendererHIP, scenes
+sc = scenes.make_scene({cfg!r})
+r = VRendererHIP(0)
+scenes.load_into(r, sc)
+r.set_strict_traversal({strict})
+F = {frames}
+r.render(frames=F, time_seed=sc["time"])     # warm-up
+r.clearBuffer()
+ts = []
+for i in range({steps}):
+    t0 = time.perf_counter()
+    r.render(frames=F, times=[sc["time"] + i * F + k for k in range(F)])
+    ts.append(time.perf_counter() - t0)
+acc = r.read_accum()
+wr, hr = (sc["width"] // 16) * 16, (sc["height"] // 16) * 16
+paths = wr * hr * 2 * F
+ts.sort()
+med = ts[len(ts) // 2]
+print(json.dumps({{"mpaths": paths / med / 1e6, "best": paths / ts[0] / 1e6,
+                   "hash": int(np.bitwise_xor.reduce(acc.view(np.uint32).reshape(-1)))}}))
+"""
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", default="C2")
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--strict", action="store_true")
+    ap.add_argument("libs", nargs="+")
+    a = ap.parse_args()
+    results = {}
+    for lib in a.libs:
+        env = dict(os.environ, VRHIP_LIB=os.path.abspath(lib))
+        code = CHILD.format(repo=REPO, cfg=a.cfg, frames=a.frames, steps=a.steps, strict=a.strict)
+        p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+        if p.returncode != 0:
+            print(f"{lib}: FAILED rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
+            if p.returncode < 0 or p.returncode > 1:
+                sys.exit(p.returncode if p.returncode > 0 else 1)
+            continue
+        res = json.loads(p.stdout.strip().splitlines()[-1])
+        results[lib] = res
+        print(f"{os.path.basename(lib):40s} {res['mpaths']:9.1f} Mpaths/s (best {res['best']:.1f})  hash {res['hash']:#x}",
+              flush=True)
+    hashes = {v["hash"] for v in results.values()}
+    print("all results identical" if len(hashes) == 1 else f"RESULTS DIFFER: {len(hashes)} distinct hashes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build libvrhip.so variants for scripts/ab.py: each argument is NAME=FLAGS,
+# e.g.  bash scripts/build_variants.sh base= w3=-DVR_MIN_WAVES_PER_SIMD=3
+# Prints VGPRs / spills of the C2 specialisation (render_kernel<32,false,9>).
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p variants
+SRC="vrenderer_pathtracer_amd/csrc/vr_kernel.hip vrenderer_pathtracer_amd/csrc/vrhip_api.cpp vrenderer_pathtracer_amd/csrc/vr_bvh.cpp"
+for spec in "$@"; do
+  name=${spec%%=*}; flags=${spec#*=}
+  ( hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -shared --offload-arch=gfx950 $flags \
+      -o variants/libvrhip_$name.so $SRC -Rpass-analysis=kernel-resource-usage 2>&1 \
+      | grep -A12 "render_kernelILi32ELb0ELj9E" | grep -E "VGPRs:|VGPRs Spill|Scratch" \
+      | sed 's/.*remark: *//;s/ \[-Rpass.*//' | tr '\n' ' ' | sed "s/^/$name: /"; echo ) &
+done
+wait

@@ -94,7 +94,7 @@ def header_symbols() -> list[str]:
 def lib():
     global _lib
     if _lib is None:
-        path = _build.LIB_PATH
+        path = os.environ.get("VRHIP_LIB", _build.LIB_PATH)   # VRHIP_LIB: A/B builds of the same ABI
         if not os.path.exists(path):
             raise RuntimeError(f"libvrhip.so not built ({path}); run vrenderer_pathtracer_amd.build.build()")
         L = ctypes.CDLL(path)

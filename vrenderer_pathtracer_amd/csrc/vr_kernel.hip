@@ -32,6 +32,11 @@ namespace vr {
 #define VR_PI 3.14159265359f        // MathHelpers.cuh:16
 #define VR_EPS 0.0000000003f        // MathHelpers.cuh:17
 
+// Scene features are tested twice: against the kernel's compile-time feature
+// set FEAT (code for absent features is compiled out, cutting VGPRs) and
+// against the launch's runtime flags.
+#define HAS(F) ((FEAT & (F)) != 0 && (p.flags & (F)) != 0)
+
 // ---- float4 with the reference's operator semantics (MathHelpers.cuh:85-196)
 __device__ __forceinline__ vr4 mk4(float x, float y, float z, float w) { vr4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
 __device__ __forceinline__ vr4 add4(vr4 a, vr4 b) { return mk4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
@@ -138,7 +143,7 @@ __device__ __forceinline__ vr4 sphere_normal(const HitRec& hr, const Ray& r) {
 // the closest hit (ties included) is unchanged.
 constexpr int kLeafCountBits = 7;
 
-template <int STACK, bool COUNT>
+template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, int* stk, Cnt& cnt)
 {
     // CudaTracerLib-style while-while traversal (PathTracer.cu:276-463)
@@ -247,12 +252,12 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
 }
 
 // intersectScene (PathTracer.cu:136-468): closest hit, attributes deferred.
-template <int STACK, bool COUNT>
+template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray& r, HitRec& hr, int* stk, Cnt& cnt)
 {
     if (COUNT) cnt.rays++;
     hr.t = 1e20f; hr.kind = HK_NONE; hr.idx = 0; hr.bu = hr.bv = 0.f; hr.su = hr.sv = 0.f;
-    if (p.flags & F_CORNELL) {
+    if HAS(F_CORNELL) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const float dist = sphere_intersect(cornell_sphere(i), r);
@@ -264,10 +269,10 @@ __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray
         const float dist = sphere_intersect(small_sphere(i), r);
         if (dist != 0.f && dist < hr.t) { hr.t = dist; hr.kind = HK_SMALL; hr.idx = i; }
     }
-    if (p.flags & F_EXAMPLE) {
+    if HAS(F_EXAMPLE) {
         const float dist = sphere_intersect(example_sphere(), r);
         if (dist != 0.f && dist < hr.t) {
-            if (p.flags & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) {
+            if (HAS(F_TEX_DIFF) || HAS(F_TEX_NORM) || HAS(F_TEX_SPEC)) {
                 // u,v from the normal left by the previous hit of this call (:202-204)
                 const vr4 sn = hr.kind == HK_NONE ? mk4(0.f, 0.f, 0.f, 0.f) : sphere_normal(hr, r);
                 hr.su = atan2_p(sn.x, sn.z) / (2.f * VR_PI) + 0.5f;
@@ -275,18 +280,19 @@ __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray
             }
             hr.t = dist; hr.kind = HK_EXAMPLE; hr.idx = 0;
         }
-    } else if (p.flags & F_MESH) {
-        traverse_mesh<STACK, COUNT>(p, r, hr, stk, cnt);
+    } else if HAS(F_MESH) {
+        traverse_mesh<STACK, COUNT, FEAT>(p, r, hr, stk, cnt);
     }
     return hr.t < 1e20f;
 }
 
 // Materialise vHitData for the final hit (the values the reference's last
 // accepted hit wrote; :160-168, :180-189, :198-266, :380-453).
+template <uint32_t FEAT>
 __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, const HitRec& hr, Hit& h)
 {
     h.tan = mk4(0.f, 0.f, 0.f, 0.f);
-    const bool view_brdf = (p.flags & F_VIEW_BRDF) != 0;
+    const bool view_brdf = HAS(F_VIEW_BRDF);
     if (hr.kind == HK_CORNELL || hr.kind == HK_SMALL) {
         const Sph s = hr.kind == HK_CORNELL ? cornell_sphere(hr.idx) : small_sphere(hr.idx);
         h.hp = add4(r.o, mul4s(r.d, hr.t));
@@ -298,11 +304,11 @@ __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, co
     } else if (hr.kind == HK_EXAMPLE) {
         const Sph s = example_sphere();
         h.hp = add4(r.o, mul4s(r.d, hr.t));
-        if ((p.flags & F_TEX_DIFF) && !view_brdf)
+        if (HAS(F_TEX_DIFF) && !view_brdf)
             h.col = p.tex[0][tex_addr(p.tex_w[0], p.tex_h[0], hr.su, hr.sv)];
         else
             h.col = mk4(s.cr, s.cg, s.cb, 0.f);
-        if (p.flags & F_TEX_NORM) {
+        if HAS(F_TEX_NORM) {
             const int a = tex_addr(p.tex_w[1], p.tex_h[1], hr.su, hr.sv);
             vr4 normal = normalize4(sub4(h.hp, mk4(s.px, s.py, s.pz, 0.f)));
             normal.w = 0.f;
@@ -319,7 +325,7 @@ __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, co
         } else {
             h.n = normalize4(sub4(h.hp, mk4(s.px, s.py, s.pz, 0.f)));
         }
-        if ((p.flags & F_TEX_SPEC) && !view_brdf)
+        if (HAS(F_TEX_SPEC) && !view_brdf)
             h.spec = p.tex[2][tex_addr(p.tex_w[2], p.tex_h[2], hr.su, hr.sv)];
         else
             h.spec = mk4(0.f, 0.f, 0.f, 0.f);
@@ -335,11 +341,11 @@ __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, co
         vr4 tangent = normalize4(add4(add4(muls4(b0, p.tangents[a]), muls4(hr.bu, p.tangents[a + 1])),
                                       muls4(hr.bv, p.tangents[a + 2])));
         tangent.w = 0.f;
-        if ((p.flags & F_TEX_DIFF) && !view_brdf)
+        if (HAS(F_TEX_DIFF) && !view_brdf)
             h.col = p.tex[0][tex_addr(p.tex_w[0], p.tex_h[0], uvx, uvy)];
         else
             h.col = mk4(1.f, 1.f, 1.f, 0.f);
-        if ((p.flags & F_TEX_NORM) && dot4(tangent, tangent) > VR_EPS) {
+        if (HAS(F_TEX_NORM) && dot4(tangent, tangent) > VR_EPS) {
             const int ta = tex_addr(p.tex_w[1], p.tex_h[1], uvx, uvy);
             vr4 normal = normalize4(add4(add4(muls4(b0, p.normals[a]), muls4(hr.bu, p.normals[a + 1])),
                                          muls4(hr.bv, p.normals[a + 2])));
@@ -351,7 +357,7 @@ __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, co
             const vr4 v0 = p.verts[a], v1 = p.verts[a + 1], v2 = p.verts[a + 2];
             h.n = normalize4(cross4(sub4(v0, v1), sub4(v0, v2)));
         }
-        if ((p.flags & F_TEX_SPEC) && !view_brdf)
+        if (HAS(F_TEX_SPEC) && !view_brdf)
             h.spec = p.tex[2][tex_addr(p.tex_w[2], p.tex_h[2], uvx, uvy)];
         else
             h.spec = mk4(0.f, 0.f, 0.f, 0.f);
@@ -423,7 +429,7 @@ __device__ __forceinline__ uint32_t hash_seeds(uint32_t& s0, uint32_t& s1) {   /
 }
 
 // trace (PathTracer.cu:597-770)
-template <int STACK, bool COUNT>
+template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ vr4 trace(const RenderParams& p, Ray ray, uint32_t& s0, uint32_t& s1, int* stk, Cnt& cnt)
 {
     vr4 accum = mk4(0.f, 0.f, 0.f, 0.f);
@@ -434,8 +440,8 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, uint32_t& s0, uint32_t& s1,
 
     for (unsigned bounces = 0; bounces < 4; bounces++) {
         HitRec hr;
-        if (!intersect_scene<STACK, COUNT>(p, ray, hr, stk, cnt)) {
-            if (!(p.flags & F_CORNELL)) {                                    // :631-648
+        if (!intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, stk, cnt)) {
+            if (!HAS(F_CORNELL)) {                                    // :631-648
                 float lx = atan2_p(ray.d.x, ray.d.z);
                 float ly = acos_p(ray.d.y);
                 lx = lx < 0 ? (float)((double)lx + 2.0 * (double)VR_PI) : lx;
@@ -453,16 +459,16 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, uint32_t& s0, uint32_t& s1,
             return mk4(0.f, 0.f, 0.f, 0.f);
         }
         Hit h;
-        fill_hit(p, ray, hr, h);
+        fill_hit<FEAT>(p, ray, hr, h);
         if (COUNT) {
             if (hr.kind == HK_MESH) {
                 cnt.attr += 24 + 48;
-                const bool vb = (p.flags & F_VIEW_BRDF) != 0;
-                cnt.tex += ((p.flags & F_TEX_DIFF) && !vb) + ((p.flags & F_TEX_SPEC) && !vb);
-                if ((p.flags & F_TEX_NORM) && dot4(h.tan, h.tan) > VR_EPS) { cnt.attr += 48; cnt.tex++; }
+                const bool vb = HAS(F_VIEW_BRDF);
+                cnt.tex += (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb);
+                if (HAS(F_TEX_NORM) && dot4(h.tan, h.tan) > VR_EPS) { cnt.attr += 48; cnt.tex++; }
             } else if (hr.kind == HK_EXAMPLE) {
-                const bool vb = (p.flags & F_VIEW_BRDF) != 0;
-                cnt.tex += ((p.flags & F_TEX_DIFF) && !vb) + ((p.flags & F_TEX_SPEC) && !vb) + ((p.flags & F_TEX_NORM) != 0);
+                const bool vb = HAS(F_VIEW_BRDF);
+                cnt.tex += (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb) + (HAS(F_TEX_NORM) != 0);
             }
         }
         if (bounces == 0) {
@@ -517,7 +523,7 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, uint32_t& s0, uint32_t& s1,
             sincos_p(rand1, &sn, &cs);
             const vr4 newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
                                                mul4s(w, __builtin_sqrtf(1 - rand2))));
-            if (p.flags & F_BRDF) {
+            if HAS(F_BRDF) {
                 const float dw = 24 * pow_p(newdir.x * newdir.x + newdir.y * newdir.y + newdir.z * newdir.z, -1.5f);
                 if (COUNT) cnt.brdf++;
                 const vr4 b = lookup_brdf(p.brdf, newdir, ray.d, h.n, h.tan);
@@ -538,8 +544,11 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, uint32_t& s0, uint32_t& s1,
 }
 
 // render (PathTracer.cu:791-868), K frames per launch.
-template <int STACK, bool COUNT>
-__global__ void __launch_bounds__(kBlockThreads) render_kernel(const RenderParams p)
+#ifndef VR_MIN_WAVES_PER_SIMD
+#define VR_MIN_WAVES_PER_SIMD 4
+#endif
+template <int STACK, bool COUNT, uint32_t FEAT>
+__global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_kernel(const RenderParams p)
 {
     __shared__ int lds_stack[STACK * kBlockThreads];
     const int tid = threadIdx.x;
@@ -568,7 +577,7 @@ __global__ void __launch_bounds__(kBlockThreads) render_kernel(const RenderParam
         unsigned char db = 0;
 #pragma unroll 1
         for (int s = 0; s < 2; ++s) {
-            const vr4 result = trace<STACK, COUNT>(p, cam, s1, s2, stk, cnt);
+            const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, s1, s2, stk, cnt);
             db = f2u8((1.f - result.w) * 255);
             io = add4(io, mul4s(result, 1.f / 2.f));
         }
@@ -645,16 +654,46 @@ __global__ void selftest_math_kernel(int fn, const float* a, const float* b, flo
 }
 
 // ---- host launchers --------------------------------------------------------
+// Feature specialisations, smallest first (BASELINE configs C1..C5); the
+// generic kernel covers everything else, deep trees and the counting variant.
+constexpr uint32_t kFeatAll = F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;
+constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH;                                   // C2, Cornell-only
+constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                              // C1
+constexpr uint32_t kFeatHdriMesh = F_MESH;                                                  // C5
+constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;        // C3
+constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
+
+template <uint32_t FEAT>
+static void launch_spec(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
+{
+    hipLaunchKernelGGL((render_kernel<32, false, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+}
+
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream)
 {
     if (n_tiles == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    if (count) {
-        if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, true>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
-        else hipLaunchKernelGGL((render_kernel<64, true>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    const uint32_t need = p.flags & kFeatAll;
+    auto covers = [need](uint32_t feat) { return (need & ~feat) == 0u; };
+    if (count || stack_depth > 32) {
+        if (count) {
+            if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, true, kFeatAll>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+            else hipLaunchKernelGGL((render_kernel<64, true, kFeatAll>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+        } else {
+            hipLaunchKernelGGL((render_kernel<64, false, kFeatAll>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+        }
+    } else if (covers(kFeatCornellMesh)) {
+        launch_spec<kFeatCornellMesh>(p, n_tiles, s);
+    } else if (covers(kFeatCornellSphere)) {
+        launch_spec<kFeatCornellSphere>(p, n_tiles, s);
+    } else if (covers(kFeatHdriMesh)) {
+        launch_spec<kFeatHdriMesh>(p, n_tiles, s);
+    } else if (covers(kFeatHdriMeshTex)) {
+        launch_spec<kFeatHdriMeshTex>(p, n_tiles, s);
+    } else if (covers(kFeatHdriBrdfSphere)) {
+        launch_spec<kFeatHdriBrdfSphere>(p, n_tiles, s);
     } else {
-        if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, false>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
-        else hipLaunchKernelGGL((render_kernel<64, false>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+        launch_spec<kFeatAll>(p, n_tiles, s);
     }
     return (int)hipGetLastError();
 }

@@ -18,32 +18,37 @@ __device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); 
 __device__ __forceinline__ uint64_t dbits(double d) { return (uint64_t)__double_as_longlong(d); }
 __device__ __forceinline__ double bitsd(uint64_t u) { return __longlong_as_double((long long)u); }
 
+// Polynomial constants are materialised into an SGPR pair at each use: gfx9
+// VOP3 has no 64-bit literal, and letting the compiler hoist ~40 of them out
+// of the bounce loop into VGPR pairs costs registers (and occupancy).
+__device__ __forceinline__ double dk(double c) { asm volatile("" : "+s"(c)); return c; }
+
 // ------------------------------------------------------------------ sincos
 __device__ __forceinline__ void sincos_p(float x, float* s, float* c)
 {
     if (!(__builtin_fabsf(x) <= 1.0e6f)) { *s = bitsf(0x7fc00000u); *c = bitsf(0x7fc00000u); return; }
     const double xd = (double)x;
-    const double k = __builtin_rint(xd * 0.6366197723675814);
-    double r = __builtin_fma(-k, 1.5707963267948966, xd);
-    r = __builtin_fma(-k, 6.123233995736766e-17, r);
+    const double k = __builtin_rint(xd * dk(0.6366197723675814));
+    double r = __builtin_fma(-k, dk(1.5707963267948966), xd);
+    r = __builtin_fma(-k, dk(6.123233995736766e-17), r);
     const double z = r * r;
-    double ps = -1.0 / 1307674368000.0;
-    ps = __builtin_fma(ps, z, 1.0 / 6227020800.0);
-    ps = __builtin_fma(ps, z, -1.0 / 39916800.0);
-    ps = __builtin_fma(ps, z, 1.0 / 362880.0);
-    ps = __builtin_fma(ps, z, -1.0 / 5040.0);
-    ps = __builtin_fma(ps, z, 1.0 / 120.0);
-    ps = __builtin_fma(ps, z, -1.0 / 6.0);
+    double ps = dk(-1.0 / 1307674368000.0);
+    ps = __builtin_fma(ps, z, dk(1.0 / 6227020800.0));
+    ps = __builtin_fma(ps, z, dk(-1.0 / 39916800.0));
+    ps = __builtin_fma(ps, z, dk(1.0 / 362880.0));
+    ps = __builtin_fma(ps, z, dk(-1.0 / 5040.0));
+    ps = __builtin_fma(ps, z, dk(1.0 / 120.0));
+    ps = __builtin_fma(ps, z, dk(-1.0 / 6.0));
     const double sd = __builtin_fma(r * z, ps, r);
-    double pc = 1.0 / 20922789888000.0;
-    pc = __builtin_fma(pc, z, -1.0 / 87178291200.0);
-    pc = __builtin_fma(pc, z, 1.0 / 479001600.0);
-    pc = __builtin_fma(pc, z, -1.0 / 3628800.0);
-    pc = __builtin_fma(pc, z, 1.0 / 40320.0);
-    pc = __builtin_fma(pc, z, -1.0 / 720.0);
-    pc = __builtin_fma(pc, z, 1.0 / 24.0);
-    pc = __builtin_fma(pc, z, -0.5);
-    const double cd = __builtin_fma(z, pc, 1.0);
+    double pc = dk(1.0 / 20922789888000.0);
+    pc = __builtin_fma(pc, z, dk(-1.0 / 87178291200.0));
+    pc = __builtin_fma(pc, z, dk(1.0 / 479001600.0));
+    pc = __builtin_fma(pc, z, dk(-1.0 / 3628800.0));
+    pc = __builtin_fma(pc, z, dk(1.0 / 40320.0));
+    pc = __builtin_fma(pc, z, dk(-1.0 / 720.0));
+    pc = __builtin_fma(pc, z, dk(1.0 / 24.0));
+    pc = __builtin_fma(pc, z, dk(-0.5));
+    const double cd = __builtin_fma(z, pc, dk(1.0));
     const float sp = (float)sd, cp = (float)cd;
     const int q = ((int)k) & 3;
     float so, co;
@@ -180,40 +185,40 @@ __device__ __forceinline__ double log2d_p(double x)
     if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
     const double t = (m - 1.0) / (m + 1.0);
     const double t2 = t * t;
-    double p = 1.0 / 23.0;
-    p = __builtin_fma(p, t2, 1.0 / 21.0);
-    p = __builtin_fma(p, t2, 1.0 / 19.0);
-    p = __builtin_fma(p, t2, 1.0 / 17.0);
-    p = __builtin_fma(p, t2, 1.0 / 15.0);
-    p = __builtin_fma(p, t2, 1.0 / 13.0);
-    p = __builtin_fma(p, t2, 1.0 / 11.0);
-    p = __builtin_fma(p, t2, 1.0 / 9.0);
-    p = __builtin_fma(p, t2, 1.0 / 7.0);
-    p = __builtin_fma(p, t2, 1.0 / 5.0);
-    p = __builtin_fma(p, t2, 1.0 / 3.0);
+    double p = dk(1.0 / 23.0);
+    p = __builtin_fma(p, t2, dk(1.0 / 21.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 19.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 17.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 15.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 13.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 11.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 9.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 7.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 5.0));
+    p = __builtin_fma(p, t2, dk(1.0 / 3.0));
     const double lnm = 2.0 * __builtin_fma(t * t2, p, t);
-    return __builtin_fma(lnm, 1.4426950408889634, (double)e);
+    return __builtin_fma(lnm, dk(1.4426950408889634), (double)e);
 }
 
 __device__ __forceinline__ double exp2d_p(double z)
 {
     const double k = __builtin_rint(z);
     const double f = z - k;
-    const double g = f * 0.6931471805599453;
-    double p = 1.0 / 6227020800.0;
-    p = __builtin_fma(p, g, 1.0 / 479001600.0);
-    p = __builtin_fma(p, g, 1.0 / 39916800.0);
-    p = __builtin_fma(p, g, 1.0 / 3628800.0);
-    p = __builtin_fma(p, g, 1.0 / 362880.0);
-    p = __builtin_fma(p, g, 1.0 / 40320.0);
-    p = __builtin_fma(p, g, 1.0 / 5040.0);
-    p = __builtin_fma(p, g, 1.0 / 720.0);
-    p = __builtin_fma(p, g, 1.0 / 120.0);
-    p = __builtin_fma(p, g, 1.0 / 24.0);
-    p = __builtin_fma(p, g, 1.0 / 6.0);
-    p = __builtin_fma(p, g, 0.5);
-    p = __builtin_fma(p, g, 1.0);
-    p = __builtin_fma(p, g, 1.0);
+    const double g = f * dk(0.6931471805599453);
+    double p = dk(1.0 / 6227020800.0);
+    p = __builtin_fma(p, g, dk(1.0 / 479001600.0));
+    p = __builtin_fma(p, g, dk(1.0 / 39916800.0));
+    p = __builtin_fma(p, g, dk(1.0 / 3628800.0));
+    p = __builtin_fma(p, g, dk(1.0 / 362880.0));
+    p = __builtin_fma(p, g, dk(1.0 / 40320.0));
+    p = __builtin_fma(p, g, dk(1.0 / 5040.0));
+    p = __builtin_fma(p, g, dk(1.0 / 720.0));
+    p = __builtin_fma(p, g, dk(1.0 / 120.0));
+    p = __builtin_fma(p, g, dk(1.0 / 24.0));
+    p = __builtin_fma(p, g, dk(1.0 / 6.0));
+    p = __builtin_fma(p, g, dk(0.5));
+    p = __builtin_fma(p, g, dk(1.0));
+    p = __builtin_fma(p, g, dk(1.0));
     const int ki = (int)k;
     const double scale = bitsd((uint64_t)(ki + 1023) << 52);
     return p * scale;
