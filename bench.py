@@ -95,6 +95,7 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     from vrenderer_pathtracer_amd import VRendererHIP, build_native, scenes
+    from vrenderer_pathtracer_amd.tiles import BandGather, WHAT_RGBA8
     build_native()
     scene = scenes.make_scene(CFG)
     W, H = scene["width"], scene["height"]
@@ -106,10 +107,7 @@ def main():
     r.set_stream(stream.cuda_stream)
     r.set_tiling(rank, world)
     owned = r.owned_rows()
-    max_owned = ((H // 16 + world - 1) // world) * 16
-    send = torch.empty(max_owned * W * 4, dtype=torch.uint8, device=dev)
-    gather = [torch.empty_like(send) for _ in range(world)] if (world > 1 and rank == 0) else None
-    recv_flat = torch.empty(world * send.numel(), dtype=torch.uint8, device=dev) if gather is not None else None
+    gather = BandGather(r, rank, world, dev, WHAT_RGBA8)
 
     # counting step (untimed): exact event counts for this rank's share
     counts = r.render_counted(frames=F, time_seed=scene["time"])
@@ -118,12 +116,7 @@ def main():
     def step(i):
         times = [scene["time"] + i * F + k for k in range(F)]
         r.render(frames=F, times=times, sync=False)
-        if world > 1:
-            r.pack_rows(0, send.data_ptr())
-            dist.gather(send, gather, dst=0)
-            if rank == 0:
-                torch.cat(gather, out=recv_flat)
-                r.unpack_rows(0, recv_flat.data_ptr(), world, send.numel())
+        gather.step()
 
     for i in range(args.warmup):
         step(i)

@@ -147,6 +147,9 @@ int vrhip_device_buffers(vrhip_ctx *ctx, void **accum, void **rgba8, void **dept
  * balance).  Seeds use global pixel coordinates, so the union of the ranks'
  * bands equals the 1-GPU image bit for bit. */
 int vrhip_set_tiling(vrhip_ctx *ctx, uint32_t rank, uint32_t n_ranks);
+/* Host-only (no device): the rows rank `rank` of n_ranks owns for an image
+ * of `height` rows, in packed order.  rows_out may be NULL to query *n_rows. */
+int vrhip_tile_rows(uint32_t height, uint32_t rank, uint32_t n_ranks, uint32_t *rows_out, uint32_t *n_rows);
 /* Number of rows this rank owns in the rendered region. */
 int vrhip_owned_rows(vrhip_ctx *ctx, uint32_t *rows);
 /* Pack this rank's owned rows (RGBA8 if what == 0, float4 accum if 1,

@@ -1,0 +1,170 @@
+"""CPU tests of the C ABI (include/vrhip.h) and the host-side BVH / layout code.
+
+No compute call needs a GPU here: the library must load, export every
+declared symbol, fail loudly (status codes, no exit) without a device, and
+its host helpers (BVH build, flattening, validation, tiling) must be right.
+"""
+import ctypes
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from vrenderer_pathtracer_amd import _native, build_flat, scenes, validate_flat
+from vrenderer_pathtracer_amd.build import LIB_PATH
+from vrenderer_pathtracer_amd.tiles import owned_rows, pack_host, unpack_host
+
+_f = ctypes.POINTER(ctypes.c_float)
+
+
+def test_library_exports_every_header_symbol(native):
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (vrhip_\w+)", out))
+    declared = set(_native.header_symbols())
+    assert declared, "no symbols parsed from include/vrhip.h"
+    assert declared <= exported, sorted(declared - exported)
+    assert native.vrhip_abi_version() == 1
+
+
+def _has_gpu(native):
+    n = ctypes.c_int(0)
+    return native.vrhip_device_count(ctypes.byref(n)) == 0 and n.value > 0
+
+
+def test_create_without_device_fails_loudly(native):
+    if _has_gpu(native):
+        pytest.skip("a GPU is visible")
+    ctx = ctypes.c_void_p()
+    rc = native.vrhip_create(0, 64, 64, ctypes.byref(ctx))
+    assert rc == -5 and not ctx.value
+    assert b"device" in native.vrhip_last_error().lower()
+
+
+def test_null_context_is_invalid(native):
+    assert native.vrhip_clear(None) == -1
+    assert native.vrhip_render(None, 1, None, 0) == -1
+    assert native.vrhip_set_fresnel(None, 0.1, 3.0) == -1
+    assert native.vrhip_destroy(None) == 0
+    assert native.vrhip_build_flat(None, None, None, None, 0, None, 0, 4, None, None, None, None, None, None,
+                                   None) == -1
+
+
+def _mesh_arrays(m):
+    return m["positions"], m["tris"]
+
+
+def test_build_flat_references_every_triangle_once(native):
+    m = scenes.torus_knot(40, 20)
+    flat = build_flat(m)
+    verts = flat["verts"]
+    term = verts[:, 0].view(np.uint32) == 0x80000000
+    tri_slots = verts[~term]
+    assert tri_slots.shape[0] == 3 * m["tris"].shape[0]
+    # each original triangle appears exactly once (object-split builder)
+    P = m["positions"]
+    key = lambda a: tuple(np.round(a, 5).reshape(-1))
+    want = sorted(key(P[t]) for t in m["tris"])
+    got = sorted(key(tri_slots[i:i + 3, :3]) for i in range(0, tri_slots.shape[0], 3))
+    assert want == got
+
+
+def test_build_flat_node_bounds_contain_children(native):
+    flat = build_flat(scenes.torus_knot(30, 12))
+    bvh, verts = flat["bvh"], flat["verts"]
+    depth, n_nodes = validate_flat(flat)
+    assert n_nodes == bvh.shape[0] // 4 and 1 <= depth <= 30
+
+    def tri_run(idx):
+        s = ~idx
+        pts = []
+        while verts[s, 0].view(np.uint32) != 0x80000000:
+            pts.append(verts[s:s + 3, :3])
+            s += 3
+        return np.concatenate(pts) if pts else np.zeros((0, 3), np.float32)
+
+    def subtree_points(idx):
+        if idx < 0:
+            return tri_run(idx)
+        n = bvh[idx:idx + 4]
+        kids = n[3, :2].view(np.int32)
+        return np.concatenate([subtree_points(int(kids[0])), subtree_points(int(kids[1]))])
+
+    for off in range(0, bvh.shape[0], 4):
+        n = bvh[off:off + 4]
+        kids = n[3, :2].view(np.int32)
+        for c in range(2):
+            lo = np.array([n[c, 0], n[c, 2], n[2, 2 * c]])
+            hi = np.array([n[c, 1], n[c, 3], n[2, 2 * c + 1]])
+            pts = subtree_points(int(kids[c]))
+            assert pts.size and (pts >= lo).all() and (pts <= hi).all()
+
+
+def test_build_flat_single_triangle_has_inner_root(native):
+    m = dict(positions=np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), tris=np.array([[0, 1, 2]], np.uint32))
+    flat = build_flat(m)
+    assert flat["bvh"].shape == (4, 4)
+    kids = flat["bvh"][3, :2].view(np.int32)
+    assert (kids < 0).all()
+    assert validate_flat(flat)[0] == 1
+
+
+def test_validate_flat_rejects_corruption(native):
+    flat = build_flat(scenes.torus_knot(20, 10))
+    bad = {k: v.copy() for k, v in flat.items()}
+    bad["bvh"][3, 0] = np.array([10 ** 6], np.int32).view(np.float32)[0]        # child out of range
+    with pytest.raises(_native.VRHIPError):
+        validate_flat(bad)
+    bad = {k: v.copy() for k, v in flat.items()}
+    bad["bvh"][3, 0] = np.array([0], np.int32).view(np.float32)[0]              # cycle back to the root
+    with pytest.raises(_native.VRHIPError):
+        validate_flat(bad)
+    bad = {k: v.copy() for k, v in flat.items()}
+    term = np.where(bad["verts"][:, 0].view(np.uint32) == 0x80000000)[0]
+    bad["verts"][term[-1], 0] = 1.0                                              # lost terminator
+    with pytest.raises(_native.VRHIPError):
+        validate_flat(bad)
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_bvh_traversal_equals_brute_force(oracle, cfg):
+    """The closest hit does not depend on the tree (no t-culling in the
+    reference traversal): BVH traversal == testing every triangle."""
+    sc = scenes.make_scene(cfg, 64, 48)
+    a, _, _, _ = po.render(sc, frames=1)
+    b, _, _, _ = po.render(sc, frames=1, brute_force=True)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_random_soup_bvh_equals_brute_force(oracle):
+    rng = np.random.default_rng(5)
+    n = 300
+    c = rng.uniform(-30, 30, (n, 1, 3))
+    P = (c + rng.normal(0, 4, (n, 3, 3))).reshape(-1, 3).astype(np.float32)
+    m = dict(positions=P, normals=np.tile([0, 0, 1], (3 * n, 1)).astype(np.float32),
+             tangents=np.tile([1, 0, 0], (3 * n, 1)).astype(np.float32),
+             uvs=rng.uniform(0, 1, (3 * n, 2)).astype(np.float32),
+             tris=np.arange(3 * n, dtype=np.uint32).reshape(-1, 3))
+    sc = scenes.make_scene("C2", 48, 32)
+    sc["mesh_flat"] = build_flat(m, max_leaf_tris=3)
+    a, _, _, _ = po.render(sc, frames=1)
+    b, _, _, _ = po.render(sc, frames=1, brute_force=True)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("H,n", [(720, 1), (720, 2), (720, 8), (1080, 8), (40, 3), (15, 2)])
+def test_tile_rows_partition(native, H, n):
+    parts = [owned_rows(H, r, n) for r in range(n)]
+    allr = np.sort(np.concatenate(parts))
+    assert np.array_equal(allr, np.arange((H // 16) * 16))
+    for r, rows in enumerate(parts):
+        assert ((rows // 16) % n == r).all()
+
+
+def test_pack_unpack_host_roundtrip(native):
+    img = np.random.default_rng(0).random((720, 64, 4)).astype(np.float32)
+    packed = [pack_host(img, r, 3) for r in range(3)]
+    out = np.zeros_like(img)
+    unpack_host(packed, 720, out)
+    assert np.array_equal(out, img)

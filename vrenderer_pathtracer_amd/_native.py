@@ -65,6 +65,7 @@ _SIGNATURES = {
     "vrhip_device_buffers": (ctypes.c_int, [_ctx, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
     "vrhip_set_tiling": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32]),
     "vrhip_owned_rows": (ctypes.c_int, [_ctx, _u32]),
+    "vrhip_tile_rows": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u32, _u32]),
     "vrhip_pack_rows": (ctypes.c_int, [_ctx, ctypes.c_int, _vp]),
     "vrhip_unpack_rows": (ctypes.c_int, [_ctx, ctypes.c_int, _vp, ctypes.c_uint32, ctypes.c_size_t]),
     "vrhip_last_kernel_ms": (ctypes.c_int, [_ctx, _f]),

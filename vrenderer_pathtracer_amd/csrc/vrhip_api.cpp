@@ -515,6 +515,18 @@ int vrhip_set_tiling(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks)
     return VRHIP_OK;
 }
 
+int vrhip_tile_rows(uint32_t height, uint32_t rank, uint32_t n_ranks, uint32_t* rows_out, uint32_t* n_rows)
+{
+    if (!n_rows || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad tiling arguments");
+    const uint32_t bands = height / 16u;
+    uint32_t n = 0;
+    for (uint32_t b = rank; b < bands; b += n_ranks)
+        for (uint32_t r = 0; r < 16u; ++r, ++n)
+            if (rows_out) rows_out[n] = b * 16u + r;
+    *n_rows = n;
+    return VRHIP_OK;
+}
+
 int vrhip_owned_rows(vrhip_ctx* c, uint32_t* rows)
 {
     if (!c || !rows) return fail(VRHIP_ERR_INVALID, "null argument");
