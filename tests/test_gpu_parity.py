@@ -162,6 +162,29 @@ def test_multi_frame_launch_equals_frame_by_frame(native):
     assert np.array_equal(a4.view(np.uint32), a1.view(np.uint32))
 
 
+@pytest.mark.parametrize("cfg,w,h", [("C2", 96, 64), ("C3", 96, 64), ("C4", 96, 64)])
+def test_strict_counts_equal_oracle_counts(native, oracle, cfg, w, h):
+    """Strict traversal visits exactly the nodes and tests exactly the
+    triangles the reference algorithm does (oracle counting mode)."""
+    sc = scenes.make_scene(cfg, w, h)
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.set_strict_traversal(True)
+    g = r.render_counted(frames=1, time_seed=sc["time"])
+    r.set_strict_traversal(False)
+    r.clearBuffer()
+    gc = r.render_counted(frames=1, time_seed=sc["time"])
+    r.cleanUp()
+    _, _, _, o = po.render(sc, frames=1, count=True, libm=po.LIBM_PORTABLE)
+    assert g["rays"] == o["rays"]
+    assert g["node_visits"] == o["node_visits"]
+    assert g["tri_tests"] == o["tri_tests"]
+    assert g["hdr_fetches"] == o["hdr_fetches"] and g["brdf_fetches"] == o["brdf_fetches"]
+    assert gc["rays"] == o["rays"] and gc["node_visits"] <= o["node_visits"]
+    print(f"{cfg}: nodes/ray strict {g['node_visits'] / g['rays']:.2f} culled {gc['node_visits'] / gc['rays']:.2f}; "
+          f"tris/ray strict {g['tri_tests'] / g['rays']:.2f} culled {gc['tri_tests'] / gc['rays']:.2f}")
+
+
 @pytest.mark.parametrize("cfg,w,h", [("C2", 160, 96), ("C3", 160, 96)])
 def test_strict_traversal_bitexact_vs_portable_oracle(native, oracle, cfg, w, h):
     sc = scenes.make_scene(cfg, w, h)
