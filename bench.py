@@ -109,8 +109,12 @@ def main():
     owned = r.owned_rows()
     gather = BandGather(r, rank, world, dev, WHAT_RGBA8)
 
-    # counting step (untimed): exact event counts for this rank's share
+    # counting step (untimed): exact event counts of the REFERENCE algorithm for
+    # this rank's share (strict traversal; the counting variant also skips the
+    # primary-hit reuse and last-bounce shortcut), i.e. the algorithmic work
+    r.set_strict_traversal(True)
     counts = r.render_counted(frames=F, time_seed=scene["time"])
+    r.set_strict_traversal(False)
     r.clearBuffer()
 
     def step(i):

@@ -367,6 +367,15 @@ __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, co
     }
 }
 
+// Emission of a hit (the only vHitData field the last bounce observes).
+__device__ __forceinline__ vr4 emission_of(const HitRec& hr) {
+    if (hr.kind == HK_CORNELL || hr.kind == HK_SMALL) {
+        const Sph s = hr.kind == HK_CORNELL ? cornell_sphere(hr.idx) : small_sphere(hr.idx);
+        return mk4(s.ex, s.ey, s.ez, 0.f);
+    }
+    return mk4(0.f, 0.f, 0.f, 0.f);
+}
+
 // MERL index maps (PathTracer.cu:473-506)
 __device__ __forceinline__ int phi_diff_index(float phi_diff) {
     if (phi_diff < 0.0) phi_diff = (float)((double)phi_diff + 3.14159265358979323846);
@@ -430,7 +439,8 @@ __device__ __forceinline__ uint32_t hash_seeds(uint32_t& s0, uint32_t& s1) {   /
 
 // trace (PathTracer.cu:597-770)
 template <int STACK, bool COUNT, uint32_t FEAT>
-__device__ vr4 trace(const RenderParams& p, Ray ray, uint32_t& s0, uint32_t& s1, int* stk, Cnt& cnt)
+__device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit0, uint32_t& s0, uint32_t& s1,
+                     int* stk, Cnt& cnt)
 {
     vr4 accum = mk4(0.f, 0.f, 0.f, 0.f);
     vr4 mask = mk4(1.f, 1.f, 1.f, 0.f);
@@ -440,7 +450,16 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, uint32_t& s0, uint32_t& s1,
 
     for (unsigned bounces = 0; bounces < 4; bounces++) {
         HitRec hr;
-        if (!intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, stk, cnt)) {
+        bool hit;
+        if (!COUNT && bounces == 0) {
+            // the camera ray is the same for both samples of every frame (no
+            // jitter, PathTracer.cu:842-844): its hit is computed once per pixel
+            hr = hr0;
+            hit = hit0;
+        } else {
+            hit = intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, stk, cnt);
+        }
+        if (!hit) {
             if (!HAS(F_CORNELL)) {                                    // :631-648
                 float lx = atan2_p(ray.d.x, ray.d.z);
                 float ly = acos_p(ray.d.y);
@@ -457,6 +476,12 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, uint32_t& s0, uint32_t& s1,
                 return accum;
             }
             return mk4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (!COUNT && bounces == 3) {
+            // last bounce: only the emission term is observable; the material
+            // branch below would only prepare a ray that is never traced
+            accum = add4(accum, mul4(mask, emission_of(hr)));
+            break;
         }
         Hit h;
         fill_hit<FEAT>(p, ray, hr, h);
@@ -569,6 +594,9 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     Ray cam;
     cam.o = p.cam_o;
     cam.d = normalize4(add4(add4(p.cam_d, mul4s(p.cx, sx)), mul4s(p.cy, sy)));
+    HitRec hr0;
+    bool hit0 = false;
+    if (!COUNT) hit0 = intersect_scene<STACK, COUNT, FEAT>(p, cam, hr0, stk, cnt);
 
     for (uint32_t f = 0; f < p.n_frames; ++f) {
         const uint32_t frame = p.first_frame + f;
@@ -577,7 +605,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
         unsigned char db = 0;
 #pragma unroll 1
         for (int s = 0; s < 2; ++s) {
-            const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, s1, s2, stk, cnt);
+            const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, stk, cnt);
             db = f2u8((1.f - result.w) * 255);
             io = add4(io, mul4s(result, 1.f / 2.f));
         }
