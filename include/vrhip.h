@@ -167,6 +167,10 @@ int vrhip_last_kernel_ms(vrhip_ctx *ctx, float *ms);
 /* Accumulated render-kernel time (ms) and launch count since the last reset,
  * from HIP events recorded around every vrhip_render on the context stream. */
 int vrhip_kernel_stats(vrhip_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
+/* Raw debug slots: [0..7] the last counted render's counters; [8..13] phase
+ * cycle totals (spheres, mesh traversal, hit materialisation, shading,
+ * tonemap, whole kernel) written only by a -DVR_TIMING diagnostic build. */
+int vrhip_debug_counters(vrhip_ctx *ctx, uint64_t out[16], int reset);
 /* Depth of the uploaded BVH and the traversal stack size in use. */
 int vrhip_bvh_info(vrhip_ctx *ctx, uint32_t *depth, uint32_t *n_nodes, uint32_t *n_slots);
 /* Evaluate the device libm on n inputs (test hook: 0 sin, 1 cos, 2 acos,

@@ -57,6 +57,7 @@ _SIGNATURES = {
                                             ctypes.POINTER(ctypes.c_uint64)]),
     "vrhip_kernel_stats": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.c_int]),
+    "vrhip_debug_counters": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "vrhip_sync": (ctypes.c_int, [_ctx]),
     "vrhip_frame_count": (ctypes.c_int, [_ctx, _u32]),
     "vrhip_read_accum": (ctypes.c_int, [_ctx, _f]),
@@ -100,6 +101,8 @@ def lib():
             raise RuntimeError(f"libvrhip.so not built ({path}); run vrenderer_pathtracer_amd.build.build()")
         L = ctypes.CDLL(path)
         for name, (res, args) in _SIGNATURES.items():
+            if path != _build.LIB_PATH and not hasattr(L, name):
+                continue   # an older A/B build may predate a diagnostics entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -111,7 +111,21 @@ struct HitRec {
     float su, sv;           // example sphere texture coords (from the stale normal)
 };
 // Per-lane event counts for the counting variant (algorithmic bytes).
-struct Cnt { uint32_t rays = 0, nodes = 0, slots = 0, tris = 0, attr = 0, tex = 0, hdr = 0, brdf = 0; };
+struct Cnt {
+    uint32_t rays = 0, nodes = 0, slots = 0, tris = 0, attr = 0, tex = 0, hdr = 0, brdf = 0;
+#ifdef VR_TIMING
+    // diagnostic build only: per-lane s_memtime cycles in spheres, mesh
+    // traversal, hit materialisation, shading, tonemap, whole kernel
+    uint64_t tm[6] = { 0, 0, 0, 0, 0, 0 };
+#endif
+};
+#ifdef VR_TIMING
+#define VR_T0(name) const uint64_t name = __builtin_amdgcn_s_memtime()
+#define VR_T1(name, slot) cnt.tm[slot] += __builtin_amdgcn_s_memtime() - name
+#else
+#define VR_T0(name) (void)0
+#define VR_T1(name, slot) (void)0
+#endif
 
 struct Hit {                // vHitData, PathTracer.cuh:17-53
     vr4 hp, n, tan, em, col, spec;
@@ -161,7 +175,7 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
     // (times a 2^-10 safety margin) cannot hold a closer triangle.  The
     // reference visits every pierced box (span end clamped to 1e20,
     // :316,322); F_STRICT restores that exactly.
-    const bool strict = (p.flags & F_STRICT) != 0;
+    const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
     const float kCull = 1.0009765625f;
     float tcull = strict ? __builtin_inff() : t * kCull;
     int best = -1;
@@ -174,21 +188,26 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
             const vr4 n1 = p.bvh[nodeAddr + 1];
             const vr4 nz = p.bvh[nodeAddr + 2];
             const vr4 ni = p.bvh[nodeAddr + 3];
-            int idx0 = __float_as_int(ni.x), idx1 = __float_as_int(ni.y);
-            const float c0lox = n0.x * ivx - odx;
-            const float c0hix = n0.y * ivx - odx;
-            const float c0loy = n0.z * ivy - ody;
-            const float c0hiy = n0.w * ivy - ody;
-            const float c0loz = nz.x * ivz - odz;
-            const float c0hiz = nz.y * ivz - odz;
-            const float c1loz = nz.z * ivz - odz;
-            const float c1hiz = nz.w * ivz - odz;
+            const int idx0 = __float_as_int(ni.x), idx1 = __float_as_int(ni.y);
+            // slab distances n*inv - o*inv (:307-322); the culled mode lets
+            // them contract to one v_fma each (more accurate)
+            auto slab = [&](float n, float iv, float od) {
+                return strict ? (n * iv - od) : __builtin_fmaf(n, iv, -od);
+            };
+            const float c0lox = slab(n0.x, ivx, odx);
+            const float c0hix = slab(n0.y, ivx, odx);
+            const float c0loy = slab(n0.z, ivy, ody);
+            const float c0hiy = slab(n0.w, ivy, ody);
+            const float c0loz = slab(nz.x, ivz, odz);
+            const float c0hiz = slab(nz.y, ivz, odz);
+            const float c1loz = slab(nz.z, ivz, odz);
+            const float c1hiz = slab(nz.w, ivz, odz);
             const float c0min = span_begin(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, 0.0f);
             const float c0max = span_end(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, 1e20f);
-            const float c1lox = n1.x * ivx - odx;
-            const float c1hix = n1.y * ivx - odx;
-            const float c1loy = n1.z * ivy - ody;
-            const float c1hiy = n1.w * ivy - ody;
+            const float c1lox = slab(n1.x, ivx, odx);
+            const float c1hix = slab(n1.y, ivx, odx);
+            const float c1loy = slab(n1.z, ivy, ody);
+            const float c1hiy = slab(n1.w, ivy, ody);
             const float c1min = span_begin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 0.0f);
             const float c1max = span_end(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 1e20f);
             // keep the child-index load in the same round trip as the bounds
@@ -196,17 +215,16 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
             const bool swp = (c1min < c0min);
             const bool tc0 = (c0max >= c0min) && (c0min <= tcull);
             const bool tc1 = (c1max >= c1min) && (c1min <= tcull);
-            if (!tc0 && !tc1) {
-                nodeAddr = stk[sp * kBlockThreads];
-                --sp;
-            } else {
-                nodeAddr = tc0 ? idx0 : idx1;
-                if (tc0 && tc1) {
-                    if (swp) { const int tmp = nodeAddr; nodeAddr = idx1; idx1 = tmp; }
-                    ++sp;
-                    stk[sp * kBlockThreads] = idx1;
-                }
-            }
+            // branch-free push/pop: near child next, far child pushed when both
+            // are hit, pop when neither is (same order as :324-343)
+            const bool both = tc0 && tc1;
+            const bool none = !tc0 && !tc1;
+            const int top = stk[sp * kBlockThreads];
+            const int nearc = (both && swp) ? idx1 : (tc0 ? idx0 : idx1);
+            const int farc = swp ? idx0 : idx1;
+            if (both) stk[(sp + 1) * kBlockThreads] = farc;
+            sp += both ? 1 : (none ? -1 : 0);
+            nodeAddr = none ? top : nearc;
             if (nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
                 leafAddr = nodeAddr;
                 nodeAddr = stk[sp * kBlockThreads];
@@ -223,20 +241,23 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
                 const vr4 v0 = p.verts[triAddr];
                 const vr4 v1 = p.verts[triAddr + 1];
                 const vr4 v2 = p.verts[triAddr + 2];
-                // intersectTriangle, RayIntersection.cuh:54-111
+                asm volatile("" ::"v"(v0.w), "v"(v1.w), "v"(v2.w));   // three dwordx4 loads, one trip
+                // intersectTriangle, RayIntersection.cuh:54-111, evaluated
+                // branch-free: every early return of the reference becomes a
+                // term of the final predicate (the values computed for a
+                // surviving triangle are the same operations in the same order)
                 const vr4 e1 = sub4(v1, v0), e2 = sub4(v2, v0);
                 const vr4 pv = cross4(r.d, e2);
                 const float det = dot4(e1, pv);
-                if (det > -VR_EPS && det < VR_EPS) continue;
                 const float inv_det = 1.f / det;
                 const vr4 tv = sub4(r.o, v0);
                 const float u = dot4(tv, pv) * inv_det;
-                if (u < 0.f || u > 1.f) continue;
                 const vr4 q = cross4(tv, e1);
                 const float v = dot4(r.d, q) * inv_det;
-                if (v < 0.f || u + v > 1.f) continue;
                 const float dist = dot4(e2, q) * inv_det;
-                if (dist > VR_EPS && dist < t) {
+                const bool ok = !(det > -VR_EPS && det < VR_EPS) && !(u < 0.f || u > 1.f) &&
+                                !(v < 0.f || u + v > 1.f);
+                if (ok && dist > VR_EPS && dist < t) {
                     t = dist; best = triAddr; bu = u; bv = v;
                     tcull = strict ? tcull : t * kCull;
                 }
@@ -256,6 +277,7 @@ template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray& r, HitRec& hr, int* stk, Cnt& cnt)
 {
     if (COUNT) cnt.rays++;
+    VR_T0(t_sph);
     hr.t = 1e20f; hr.kind = HK_NONE; hr.idx = 0; hr.bu = hr.bv = 0.f; hr.su = hr.sv = 0.f;
     if HAS(F_CORNELL) {
 #pragma unroll
@@ -281,8 +303,13 @@ __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray
             hr.t = dist; hr.kind = HK_EXAMPLE; hr.idx = 0;
         }
     } else if HAS(F_MESH) {
+        VR_T1(t_sph, 0);
+        VR_T0(t_mesh);
         traverse_mesh<STACK, COUNT, FEAT>(p, r, hr, stk, cnt);
+        VR_T1(t_mesh, 1);
+        return hr.t < 1e20f;
     }
+    VR_T1(t_sph, 0);
     return hr.t < 1e20f;
 }
 
@@ -484,7 +511,9 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit
             break;
         }
         Hit h;
+        VR_T0(t_fill);
         fill_hit<FEAT>(p, ray, hr, h);
+        VR_T1(t_fill, 2);
         if (COUNT) {
             if (hr.kind == HK_MESH) {
                 cnt.attr += 24 + 48;
@@ -503,6 +532,7 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit
         accum = add4(accum, mul4(mask, h.em));
         ray.o = h.hp;
         const vr4 normal = h.n;
+        VR_T0(t_shade);
         if (h.type == 0) {                                                   // :671-676
             ray.d = sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d)));
             ray.o = add4(ray.o, mul4s(normal, 0.05f));
@@ -563,6 +593,7 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit
             ray.o = add4(ray.o, mul4s(normal, 0.05f));
             ray.d = newdir;
         }
+        VR_T1(t_shade, 3);
     }
     accum.w = depth;
     return accum;
@@ -586,6 +617,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     if (x >= p.wr || y >= p.hr) return;   // never true for a valid launch
     int* stk = lds_stack + tid;
     Cnt cnt;
+    VR_T0(t_kernel);
 
     const uint32_t ind = x + y * p.W;
     vr4 io = p.first_frame == 1 ? mk4(0.f, 0.f, 0.f, 0.f) : p.accum[ind];
@@ -611,6 +643,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
         }
         u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
         p.depth[ind] = dv;
+        VR_T0(t_tone);
         const float coef = 1.f / (float)frame;
         const vr4 sc = mul4s(io, coef);
         const float inv_gamma = 1.f / 2.2f;
@@ -620,8 +653,21 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
         c.z = f2u8(pow_p(clampf(sc.z, 0.f, 1.f), inv_gamma) * 255);
         c.w = 0xff;
         p.rgba[ind] = c;
+        VR_T1(t_tone, 4);
     }
     p.accum[ind] = io;
+#ifdef VR_TIMING
+    VR_T1(t_kernel, 5);
+    if (p.counters) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            unsigned long long x = cnt.tm[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+            if (lane == 0) atomicAdd(p.counters + 8 + k, x);
+        }
+    }
+#endif
     if (COUNT) {
         // one wave-level reduction and one 64-bit atomic per counter per wave
         uint32_t v[8] = { cnt.rays, cnt.nodes, cnt.slots, cnt.tris, cnt.attr, cnt.tex, cnt.hdr, cnt.brdf };
@@ -684,7 +730,8 @@ __global__ void selftest_math_kernel(int fn, const float* a, const float* b, flo
 // ---- host launchers --------------------------------------------------------
 // Feature specialisations, smallest first (BASELINE configs C1..C5); the
 // generic kernel covers everything else, deep trees and the counting variant.
-constexpr uint32_t kFeatAll = F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;
+constexpr uint32_t kFeatAll =
+    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT;
 constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH;                                   // C2, Cornell-only
 constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                              // C1
 constexpr uint32_t kFeatHdriMesh = F_MESH;                                                  // C5

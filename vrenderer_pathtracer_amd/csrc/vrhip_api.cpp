@@ -366,6 +366,17 @@ int vrhip_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
     return VRHIP_OK;
 }
 
+constexpr int kDebugSlots = 16;
+
+static int ensure_counters(vrhip_ctx* c)
+{
+    if (!c->counters) {
+        HIP_TRY(hipMalloc((void**)&c->counters, sizeof(unsigned long long) * kDebugSlots));
+        HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kDebugSlots, c->stream));
+    }
+    return VRHIP_OK;
+}
+
 static int account_pending(vrhip_ctx* c)
 {
     if (!c->pending) return VRHIP_OK;
@@ -418,10 +429,14 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     const uint32_t n_tiles = (owned_rows_of(c, c->rank) / 16u) * p.tiles_x;
     const int stack = c->bvh_depth <= 30 ? 32 : 64;
     if (count) {
-        if (!c->counters) HIP_TRY(hipMalloc((void**)&c->counters, sizeof(unsigned long long) * vr::kCounters));
+        if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
         p.counters = c->counters;
     }
+#ifdef VR_TIMING
+    if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
+    p.counters = c->counters;   // diagnostic build: phase timers in slots 8..13
+#endif
     if ((rc = account_pending(c)) != VRHIP_OK) return rc;
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     uint32_t done = 0;
@@ -457,6 +472,19 @@ int vrhip_render_counted(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times,
     HIP_TRY(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int i = 0; i < vr::kCounters; ++i) counters[i] = (uint64_t)h[i];
+    return VRHIP_OK;
+}
+
+int vrhip_debug_counters(vrhip_ctx* c, uint64_t out[16], int reset)
+{
+    if (!c || !out) return fail(VRHIP_ERR_INVALID, "null argument");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
+    unsigned long long h[kDebugSlots] = {};
+    HIP_TRY(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < kDebugSlots; ++i) out[i] = (uint64_t)h[i];
+    if (reset) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(h), c->stream));
     return VRHIP_OK;
 }
 
