@@ -8,9 +8,11 @@ mkdir -p variants
 SRC="vrenderer_pathtracer_amd/csrc/vr_kernel.hip vrenderer_pathtracer_amd/csrc/vrhip_api.cpp vrenderer_pathtracer_amd/csrc/vr_bvh.cpp"
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
-  ( hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -shared --offload-arch=gfx950 $flags \
-      -o variants/libvrhip_$name.so $SRC -Rpass-analysis=kernel-resource-usage 2>&1 \
-      | grep -A12 "render_kernelILi32ELb0ELj9E" | grep -E "VGPRs:|VGPRs Spill|Scratch" \
-      | sed 's/.*remark: *//;s/ \[-Rpass.*//' | tr '\n' ' ' | sed "s/^/$name: /"; echo ) &
+  ( rm -f variants/libvrhip_$name.so
+    hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -shared --offload-arch=gfx950 $flags \
+      -o variants/libvrhip_$name.so $SRC -Rpass-analysis=kernel-resource-usage > variants/$name.log 2>&1
+    grep -A12 "render_kernelILi32ELb0ELj9E" variants/$name.log | grep -E "VGPRs:|VGPRs Spill|Scratch" \
+      | sed 's/.*remark: *//;s/ \[-Rpass.*//' | tr '\n' ' ' | sed "s/^/$name: /"; echo
+    [ -f variants/libvrhip_$name.so ] || { grep -m5 error: variants/$name.log; echo "$name: BUILD FAILED"; } ) &
 done
 wait

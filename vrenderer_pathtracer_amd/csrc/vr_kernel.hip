@@ -187,8 +187,8 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
             const vr4 n0 = p.bvh[nodeAddr + 0];
             const vr4 n1 = p.bvh[nodeAddr + 1];
             const vr4 nz = p.bvh[nodeAddr + 2];
-            const vr4 ni = p.bvh[nodeAddr + 3];
-            const int idx0 = __float_as_int(ni.x), idx1 = __float_as_int(ni.y);
+            const int2 ni = *reinterpret_cast<const int2*>(p.bvh + nodeAddr + 3);   // 8 of the 16 bytes are used
+            const int idx0 = ni.x, idx1 = ni.y;
             // slab distances n*inv - o*inv (:307-322); the culled mode lets
             // them contract to one v_fma each (more accurate)
             auto slab = [&](float n, float iv, float od) {
@@ -238,10 +238,11 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
             for (int k = lv >> kLeafCountBits; k < kend; ++k) {
                 const int triAddr = 3 * k;
                 if (COUNT) cnt.tris++;
-                const vr4 v0 = p.verts[triAddr];
-                const vr4 v1 = p.verts[triAddr + 1];
-                const vr4 v2 = p.verts[triAddr + 2];
-                asm volatile("" ::"v"(v0.w), "v"(v1.w), "v"(v2.w));   // three dwordx4 loads, one trip
+                const vr3 a0 = p.verts[triAddr], a1 = p.verts[triAddr + 1], a2 = p.verts[triAddr + 2];
+                asm volatile("" ::"v"(a0.x), "v"(a1.x), "v"(a2.x));   // three dwordx3 loads, one trip
+                const vr4 v0 = mk4(a0.x, a0.y, a0.z, 0.f);
+                const vr4 v1 = mk4(a1.x, a1.y, a1.z, 0.f);
+                const vr4 v2 = mk4(a2.x, a2.y, a2.z, 0.f);
                 // intersectTriangle, RayIntersection.cuh:54-111, evaluated
                 // branch-free: every early return of the reference becomes a
                 // term of the final predicate (the values computed for a
@@ -381,7 +382,8 @@ __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, co
             const vr4 nm = normalize4(sub4(muls4(2.f, p.tex[1][ta]), mk4(1.f, 1.f, 1.f, 0.f)));
             h.n = normalize4(tbn_mul(tangent, bitangent, normal, nm));
         } else {
-            const vr4 v0 = p.verts[a], v1 = p.verts[a + 1], v2 = p.verts[a + 2];
+            const vr3 a0 = p.verts[a], a1 = p.verts[a + 1], a2 = p.verts[a + 2];
+            const vr4 v0 = mk4(a0.x, a0.y, a0.z, 0.f), v1 = mk4(a1.x, a1.y, a1.z, 0.f), v2 = mk4(a2.x, a2.y, a2.z, 0.f);
             h.n = normalize4(cross4(sub4(v0, v1), sub4(v0, v2)));
         }
         if (HAS(F_TEX_SPEC) && !view_brdf)

@@ -9,6 +9,7 @@ namespace vr {
 // float4 / float2 with the reference's memory layout (16 B / 8 B aligned)
 struct alignas(16) vr4 { float x, y, z, w; };
 struct alignas(8) vr2 { float x, y; };
+struct vr3 { float x, y, z; };        // packed 12 B (triangle vertices: 3 x dwordx3 per test)
 struct alignas(4) u8x4 { unsigned char x, y, z, w; };
 
 enum Flags : uint32_t {
@@ -39,7 +40,7 @@ struct RenderParams {
     uint32_t rank, nranks;           // interleaved 16-row band sharding
     uint32_t first_frame, n_frames;
     const vr4* bvh;
-    const vr4* verts;
+    const vr3* verts;                // 3 vertices per triangle, compact leaf order
     const vr4* normals;
     const vr4* tangents;
     const vr2* uvs;

@@ -19,6 +19,7 @@
 #include "vr_bvh.hpp"
 #include "vr_params.hpp"
 
+using vr::vr3;
 using vr::vr2;
 using vr::vr4;
 
@@ -57,7 +58,7 @@ struct vrhip_ctx {
     bool cornell = false, example = false, view_brdf = false;
     bool strict = false;          // exact reference traversal (no t-culling)
     // mesh
-    vr4* bvh = nullptr; vr4* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
+    vr4* bvh = nullptr; vr3* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
     uint32_t bvh_depth = 0, bvh_nodes = 0;
     bool mesh = false;
@@ -110,7 +111,8 @@ uint32_t owned_rows_of(const vrhip_ctx* c, uint32_t rank)
 // reference flattening (src/vRendererCuda.cpp:204-279) so the triangles a
 // leaf tests, and their order, are exactly the reference's.
 struct DeviceMesh {
-    std::vector<vr4> nodes, tris, normals, tangents;
+    std::vector<vr4> nodes, normals, tangents;
+    std::vector<vr3> tris;           // packed 12 B vertices (vertex .w never reaches a result)
     std::vector<vr2> uvs;
 };
 
@@ -145,7 +147,7 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
                     std::memcpy(&b, &verts[s].x, 4);
                     if (b == 0x80000000u) break;
                     for (int k = 0; k < 3; ++k) {
-                        dm.tris.push_back(verts[s + k]);
+                        dm.tris.push_back(vr3{ verts[s + k].x, verts[s + k].y, verts[s + k].z });
                         dm.normals.push_back(normals[s + k]);
                         dm.tangents.push_back(tangents[s + k]);
                         dm.uvs.push_back(uvs[s + k]);
@@ -161,7 +163,12 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
             std::memcpy(&idxf[ch], &code, 4);
         }
     }
-    if (dm.tris.empty()) { dm.tris.push_back(vr4{ 0, 0, 0, 0 }); dm.normals = dm.tangents = dm.tris; dm.uvs.push_back(vr2{ 0, 0 }); }
+    if (dm.tris.empty()) {
+        dm.tris.push_back(vr3{ 0, 0, 0 });
+        dm.normals.push_back(vr4{ 0, 0, 0, 0 });
+        dm.tangents = dm.normals;
+        dm.uvs.push_back(vr2{ 0, 0 });
+    }
     return true;
 }
 
@@ -295,7 +302,7 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     int rc = set_device(c); if (rc) return rc;
     const size_t nt = dm.tris.size();
     if ((rc = upload(c, c->bvh, dm.nodes.data(), dm.nodes.size() * 16))) return rc;
-    if ((rc = upload(c, c->verts, dm.tris.data(), nt * 16))) return rc;
+    if ((rc = upload(c, c->verts, dm.tris.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->normals, dm.normals.data(), nt * 16))) return rc;
     if ((rc = upload(c, c->tangents, dm.tangents.data(), nt * 16))) return rc;
     if ((rc = upload(c, c->uvs, dm.uvs.data(), nt * 8))) return rc;
