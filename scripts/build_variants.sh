@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build libvrhip.so variants for scripts/ab.py: each argument is NAME=FLAGS,
 # e.g.  bash scripts/build_variants.sh base= w3=-DVR_MIN_WAVES_PER_SIMD=3
-# Prints VGPRs / spills of the C2 specialisation (render_kernel<32,false,9>).
+# Prints VGPRs / spills of the C2 specialisation (render_kernel<16,false,9>).
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p variants
@@ -11,7 +11,7 @@ for spec in "$@"; do
   ( rm -f variants/libvrhip_$name.so
     hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -shared --offload-arch=gfx950 $flags \
       -o variants/libvrhip_$name.so $SRC -Rpass-analysis=kernel-resource-usage > variants/$name.log 2>&1
-    grep -A12 "render_kernelILi32ELb0ELj9E" variants/$name.log | grep -E "VGPRs:|VGPRs Spill|Scratch" \
+    grep -A12 "render_kernelILi..ELb0ELj9E" variants/$name.log | grep -E "VGPRs:|VGPRs Spill|Scratch" \
       | sed 's/.*remark: *//;s/ \[-Rpass.*//' | tr '\n' ' ' | sed "s/^/$name: /"; echo
     [ -f variants/libvrhip_$name.so ] || { grep -m5 error: variants/$name.log; echo "$name: BUILD FAILED"; } ) &
 done

@@ -157,9 +157,51 @@ __device__ __forceinline__ vr4 sphere_normal(const HitRec& hr, const Ray& r) {
 // the closest hit (ties included) is unchanged.
 constexpr int kLeafCountBits = 7;
 
+// Per-block LDS: the traversal stacks (entry-major, one column per thread)
+// and a copy of the first nodes of the area-ordered node array (rows 0-2 and
+// the two child indices, 56 B per node).  The node cache takes what is left
+// of a 40 KB budget, so four blocks (16 waves) still fit a CU's 160 KB.
+#ifndef VR_LDS_BUDGET
+#define VR_LDS_BUDGET (40960 - 256)
+#endif
+constexpr int kLdsBudget = VR_LDS_BUDGET;
+constexpr int cache_nodes(int stack) { return (kLdsBudget - stack * kBlockThreads * 4) / 56 > 0 ?
+                                              (kLdsBudget - stack * kBlockThreads * 4) / 56 : 1; }
+// Raw buffer loads for the node and triangle arrays: a 32-bit lane offset
+// against an SGPR descriptor (bounds-checked, no 64-bit address math), and an
+// explicit width per fetch (16 B node rows, 8 B child indices, 12 B vertices).
+typedef unsigned int vr_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int vr_u32x3 __attribute__((ext_vector_type(3)));
+typedef unsigned int vr_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ vr4 buf_load4(__amdgpu_buffer_rsrc_t b, int off) {
+    const vr_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, 0);
+    return mk4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ vr3 buf_load3(__amdgpu_buffer_rsrc_t b, int off) {
+    const vr_u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(b, off, 0, 0);
+    return vr3{ __uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z) };
+}
+__device__ __forceinline__ int2 buf_load2i(__amdgpu_buffer_rsrc_t b, int off) {
+    const vr_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(b, off, 0, 0);
+    return make_int2((int)v.x, (int)v.y);
+}
+
+struct Lds {
+    int* stk;                 // this thread's column of the stack
+    const vr4* nodes;         // 3 rows per cached node
+    const int2* idx;          // child indices per cached node
+    int n_cached;             // nodes [0, n_cached) are read from LDS
+};
+
 template <int STACK, bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, int* stk, Cnt& cnt)
+__device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
 {
+    int* stk = L.stk;
+    const __amdgpu_buffer_rsrc_t nbuf = buf_rsrc(p.bvh, p.n_nodes * 64u);
+    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, p.n_tris * 36u);
     // CudaTracerLib-style while-while traversal (PathTracer.cu:276-463)
     const int Sentinel = 0x76543210;
     int sp = 0;
@@ -184,10 +226,26 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
     while (nodeAddr != Sentinel) {
         while ((unsigned)nodeAddr < (unsigned)Sentinel) {
             if (COUNT) cnt.nodes++;
-            const vr4 n0 = p.bvh[nodeAddr + 0];
-            const vr4 n1 = p.bvh[nodeAddr + 1];
-            const vr4 nz = p.bvh[nodeAddr + 2];
-            const int2 ni = *reinterpret_cast<const int2*>(p.bvh + nodeAddr + 3);   // 8 of the 16 bytes are used
+            vr4 n0, n1, nz;
+            int2 ni;
+            const int node = nodeAddr >> 2;
+            // wave-uniform choice: a diverged wave would pay both round trips
+#ifdef VR_LANE_CACHE
+            if (node < L.n_cached) {
+#else
+            if (__ballot(node >= L.n_cached) == 0ull) {
+#endif
+                n0 = L.nodes[3 * node + 0];
+                n1 = L.nodes[3 * node + 1];
+                nz = L.nodes[3 * node + 2];
+                ni = L.idx[node];
+            } else {
+                const int off = nodeAddr * 16;                    // byte offset of the node
+                n0 = buf_load4(nbuf, off);
+                n1 = buf_load4(nbuf, off + 16);
+                nz = buf_load4(nbuf, off + 32);
+                ni = buf_load2i(nbuf, off + 48);                  // 8 of the row's 16 bytes are used
+            }
             const int idx0 = ni.x, idx1 = ni.y;
             // slab distances n*inv - o*inv (:307-322); the culled mode lets
             // them contract to one v_fma each (more accurate)
@@ -238,7 +296,8 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
             for (int k = lv >> kLeafCountBits; k < kend; ++k) {
                 const int triAddr = 3 * k;
                 if (COUNT) cnt.tris++;
-                const vr3 a0 = p.verts[triAddr], a1 = p.verts[triAddr + 1], a2 = p.verts[triAddr + 2];
+                const int toff = k * 36;
+                const vr3 a0 = buf_load3(tbuf, toff), a1 = buf_load3(tbuf, toff + 12), a2 = buf_load3(tbuf, toff + 24);
                 asm volatile("" ::"v"(a0.x), "v"(a1.x), "v"(a2.x));   // three dwordx3 loads, one trip
                 const vr4 v0 = mk4(a0.x, a0.y, a0.z, 0.f);
                 const vr4 v1 = mk4(a1.x, a1.y, a1.z, 0.f);
@@ -275,7 +334,7 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
 
 // intersectScene (PathTracer.cu:136-468): closest hit, attributes deferred.
 template <int STACK, bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray& r, HitRec& hr, int* stk, Cnt& cnt)
+__device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
 {
     if (COUNT) cnt.rays++;
     VR_T0(t_sph);
@@ -306,7 +365,7 @@ __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray
     } else if HAS(F_MESH) {
         VR_T1(t_sph, 0);
         VR_T0(t_mesh);
-        traverse_mesh<STACK, COUNT, FEAT>(p, r, hr, stk, cnt);
+        traverse_mesh<STACK, COUNT, FEAT>(p, r, hr, L, cnt);
         VR_T1(t_mesh, 1);
         return hr.t < 1e20f;
     }
@@ -469,7 +528,7 @@ __device__ __forceinline__ uint32_t hash_seeds(uint32_t& s0, uint32_t& s1) {   /
 // trace (PathTracer.cu:597-770)
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit0, uint32_t& s0, uint32_t& s1,
-                     int* stk, Cnt& cnt)
+                     const Lds& L, Cnt& cnt)
 {
     vr4 accum = mk4(0.f, 0.f, 0.f, 0.f);
     vr4 mask = mk4(1.f, 1.f, 1.f, 0.f);
@@ -486,7 +545,7 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit
             hr = hr0;
             hit = hit0;
         } else {
-            hit = intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, stk, cnt);
+            hit = intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, L, cnt);
         }
         if (!hit) {
             if (!HAS(F_CORNELL)) {                                    // :631-648
@@ -608,8 +667,25 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit
 template <int STACK, bool COUNT, uint32_t FEAT>
 __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_kernel(const RenderParams p)
 {
+    constexpr int CN = cache_nodes(STACK);
     __shared__ int lds_stack[STACK * kBlockThreads];
+    __shared__ vr4 lds_nodes[3 * CN];
+    __shared__ int2 lds_idx[CN];
     const int tid = threadIdx.x;
+    Lds L;
+    L.stk = lds_stack + tid;
+    L.nodes = lds_nodes;
+    L.idx = lds_idx;
+    L.n_cached = 0;
+#ifndef VR_NO_NODE_CACHE
+    if (HAS(F_MESH)) {
+        L.n_cached = (int)(p.n_nodes < (uint32_t)CN ? p.n_nodes : (uint32_t)CN);
+        for (int i = tid; i < 3 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh[(i / 3) * 4 + i % 3];
+        for (int i = tid; i < L.n_cached; i += kBlockThreads)
+            lds_idx[i] = *reinterpret_cast<const int2*>(p.bvh + 4 * i + 3);
+        __syncthreads();
+    }
+#endif
     const int wave = tid >> 6, lane = tid & 63;
     const uint32_t band_local = blockIdx.x / p.tiles_x;
     const uint32_t tile_x = blockIdx.x - band_local * p.tiles_x;
@@ -617,7 +693,6 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
     const uint32_t y = band * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     if (x >= p.wr || y >= p.hr) return;   // never true for a valid launch
-    int* stk = lds_stack + tid;
     Cnt cnt;
     VR_T0(t_kernel);
 
@@ -630,7 +705,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     cam.d = normalize4(add4(add4(p.cam_d, mul4s(p.cx, sx)), mul4s(p.cy, sy)));
     HitRec hr0;
     bool hit0 = false;
-    if (!COUNT) hit0 = intersect_scene<STACK, COUNT, FEAT>(p, cam, hr0, stk, cnt);
+    if (!COUNT) hit0 = intersect_scene<STACK, COUNT, FEAT>(p, cam, hr0, L, cnt);
 
     for (uint32_t f = 0; f < p.n_frames; ++f) {
         const uint32_t frame = p.first_frame + f;
@@ -639,7 +714,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
         unsigned char db = 0;
 #pragma unroll 1
         for (int s = 0; s < 2; ++s) {
-            const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, stk, cnt);
+            const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, L, cnt);
             db = f2u8((1.f - result.w) * 255);
             io = add4(io, mul4s(result, 1.f / 2.f));
         }
@@ -741,9 +816,15 @@ constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_S
 constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
 
 template <uint32_t FEAT>
-static void launch_spec(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
+static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
 {
-    hipLaunchKernelGGL((render_kernel<32, false, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+#ifndef VR_MIN_SPEC_STACK
+#define VR_MIN_SPEC_STACK 16
+#endif
+    if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
+        hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL((render_kernel<32, false, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
 }
 
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream)
@@ -760,17 +841,17 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool
             hipLaunchKernelGGL((render_kernel<64, false, kFeatAll>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
         }
     } else if (covers(kFeatCornellMesh)) {
-        launch_spec<kFeatCornellMesh>(p, n_tiles, s);
+        launch_spec<kFeatCornellMesh>(p, n_tiles, stack_depth, s);
     } else if (covers(kFeatCornellSphere)) {
-        launch_spec<kFeatCornellSphere>(p, n_tiles, s);
+        launch_spec<kFeatCornellSphere>(p, n_tiles, stack_depth, s);
     } else if (covers(kFeatHdriMesh)) {
-        launch_spec<kFeatHdriMesh>(p, n_tiles, s);
+        launch_spec<kFeatHdriMesh>(p, n_tiles, stack_depth, s);
     } else if (covers(kFeatHdriMeshTex)) {
-        launch_spec<kFeatHdriMeshTex>(p, n_tiles, s);
+        launch_spec<kFeatHdriMeshTex>(p, n_tiles, stack_depth, s);
     } else if (covers(kFeatHdriBrdfSphere)) {
-        launch_spec<kFeatHdriBrdfSphere>(p, n_tiles, s);
+        launch_spec<kFeatHdriBrdfSphere>(p, n_tiles, stack_depth, s);
     } else {
-        launch_spec<kFeatAll>(p, n_tiles, s);
+        launch_spec<kFeatAll>(p, n_tiles, stack_depth, s);
     }
     return (int)hipGetLastError();
 }

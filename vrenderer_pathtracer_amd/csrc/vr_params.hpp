@@ -40,7 +40,9 @@ struct RenderParams {
     uint32_t rank, nranks;           // interleaved 16-row band sharding
     uint32_t first_frame, n_frames;
     const vr4* bvh;
+    uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
     const vr3* verts;                // 3 vertices per triangle, compact leaf order
+    uint32_t n_tris;                 // triangles in verts/normals/tangents/uvs
     const vr4* normals;
     const vr4* tangents;
     const vr2* uvs;

@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <queue>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -60,7 +61,7 @@ struct vrhip_ctx {
     // mesh
     vr4* bvh = nullptr; vr3* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
-    uint32_t bvh_depth = 0, bvh_nodes = 0;
+    uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0;
     bool mesh = false;
     // environment / textures / brdf
     vr4* hdr = nullptr; uint32_t hdr_w = 0, hdr_h = 0;
@@ -118,6 +119,53 @@ struct DeviceMesh {
 
 constexpr int kLeafCountBits = 7;
 
+// Renumbers the inner nodes so that node i is the i-th largest box by surface
+// area (a parent always precedes its children; the root stays at 0).  The
+// kernel keeps a prefix of this array in LDS: the boxes a random ray is most
+// likely to enter.  Only addresses change -- every node keeps its boxes and
+// child order, so the traversal visits the same nodes in the same order.
+void order_nodes_by_area(DeviceMesh& dm)
+{
+    const size_t n = dm.nodes.size() / 4;
+    if (n == 0) return;
+    auto child_area = [&](size_t node, int ch) {
+        const vr4& a = dm.nodes[4 * node + ch];            // x and y extents of child ch
+        const vr4& z = dm.nodes[4 * node + 2];
+        const float dx = a.y - a.x, dy = a.w - a.z, dz = ch ? z.w - z.z : z.y - z.x;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    std::vector<int32_t> newoff(n, -1);
+    std::vector<size_t> order;
+    order.reserve(n);
+    std::priority_queue<std::pair<float, int64_t>> pq;   // (area, -node): ties by address
+    pq.push({ INFINITY, 0 });
+    newoff[0] = 0;
+    while (!pq.empty()) {
+        const size_t node = (size_t)(-pq.top().second);
+        pq.pop();
+        newoff[node] = (int32_t)(4 * order.size());
+        order.push_back(node);
+        for (int ch = 0; ch < 2; ++ch) {
+            int32_t idx;
+            std::memcpy(&idx, &dm.nodes[4 * node + 3].x + ch, 4);
+            if (idx < 0 || newoff[idx / 4] != -1) continue;
+            newoff[idx / 4] = -2;                          // queued
+            pq.push({ child_area(node, ch), -(int64_t)(idx / 4) });
+        }
+    }
+    std::vector<vr4> out(4 * order.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+        for (int r = 0; r < 4; ++r) out[4 * i + r] = dm.nodes[4 * order[i] + r];
+        for (int ch = 0; ch < 2; ++ch) {
+            float* slot = &out[4 * i + 3].x + ch;
+            int32_t idx;
+            std::memcpy(&idx, slot, 4);
+            if (idx >= 0) std::memcpy(slot, &newoff[idx / 4], 4);
+        }
+    }
+    dm.nodes.swap(out);
+}
+
 bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const vr4* normals,
                       const vr4* tangents, const vr2* uvs, DeviceMesh& dm, std::string& why)
 {
@@ -163,6 +211,9 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
             std::memcpy(&idxf[ch], &code, 4);
         }
     }
+#ifndef VR_NO_AREA_ORDER
+    order_nodes_by_area(dm);
+#endif
     if (dm.tris.empty()) {
         dm.tris.push_back(vr3{ 0, 0, 0 });
         dm.normals.push_back(vr4{ 0, 0, 0, 0 });
@@ -309,6 +360,8 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_bvh = n_bvh_f4; c->n_slots = n_slots;
     c->bvh_depth = depth; c->bvh_nodes = nodes;
+    c->dev_nodes = (uint32_t)(dm.nodes.size() / 4);
+    c->dev_tris = (uint32_t)(nt / 3);
     c->mesh = true;
     return VRHIP_OK;
 }
@@ -428,13 +481,13 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.flags = f;
     p.tiles_x = p.wr / 16u;
     p.rank = c->rank; p.nranks = c->nranks;
-    p.bvh = c->bvh; p.verts = c->verts; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
+    p.bvh = c->bvh; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
     p.hdr = c->hdr; p.hdr_w = c->hdr_w; p.hdr_h = c->hdr_h;
     for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
     p.brdf = c->brdf;
     p.accum = c->accum; p.rgba = c->rgba; p.depth = c->depth;
     const uint32_t n_tiles = (owned_rows_of(c, c->rank) / 16u) * p.tiles_x;
-    const int stack = c->bvh_depth <= 30 ? 32 : 64;
+    const int stack = c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 30 ? 32 : 64;   // entries needed: depth + 1
     if (count) {
         if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
