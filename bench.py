@@ -9,9 +9,10 @@ HBM), ending with the tile gather to rank 0 when N > 1.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F]
 
-N > 1: one process per GPU (torch.distributed.run), 16-row bands dealt
-round-robin, each rank renders its bands of every frame, then one RCCL gather
-(torch.distributed over "nccl" = RCCL) of the RGBA8 tiles to rank 0 per step.
+N > 1: one process per GPU (torch.distributed.run), 16x16 pixel
+tiles dealt round-robin, each rank renders its tiles of every frame, then one
+RCCL gather (torch.distributed over "nccl" = RCCL) of the RGBA8 tiles to rank
+0 per step.
 Strong scaling: the frame size is fixed.
 
 Prints ONE JSON line (rank 0).  value = total paths of all ranks / max-over-
@@ -77,7 +78,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames-per-step", type=int, default=8)
+    ap.add_argument("--frames-per-step", type=int, default=16)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -95,7 +96,7 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     from vrenderer_pathtracer_amd import VRendererHIP, build_native, scenes
-    from vrenderer_pathtracer_amd.tiles import BandGather, WHAT_RGBA8
+    from vrenderer_pathtracer_amd.tiles import TileGather, WHAT_RGBA8
     build_native()
     scene = scenes.make_scene(CFG)
     W, H = scene["width"], scene["height"]
@@ -106,8 +107,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     r.set_stream(stream.cuda_stream)
     r.set_tiling(rank, world)
-    owned = r.owned_rows()
-    gather = BandGather(r, rank, world, dev, WHAT_RGBA8)
+    owned = r.owned_pixels()
+    gather = TileGather(r, rank, world, dev, WHAT_RGBA8)
 
     # counting step (untimed): exact event counts of the REFERENCE algorithm for
     # this rank's share (strict traversal; the counting variant also skips the
@@ -147,7 +148,7 @@ def main():
     cvec = torch.tensor([counts[k] for k in keys] + [owned], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(cvec)
-    tot = {k: float(v) for k, v in zip(keys + ["owned_rows"], cvec.tolist())}
+    tot = {k: float(v) for k, v in zip(keys + ["owned_pixels"], cvec.tolist())}
 
     wr = (W // 16) * 16
     hr = (H // 16) * 16
@@ -159,8 +160,8 @@ def main():
 
     if rank == 0:
         # roofline of the render kernel on rank 0 (its own share per launch)
-        own_paths = owned * wr * 2 * F
-        bytes_per_launch = algorithmic_bytes(counts, own_paths, owned * wr * F)
+        own_paths = owned * 2 * F
+        bytes_per_launch = algorithmic_bytes(counts, own_paths, owned * F)
         avg_launch_s = (kms / 1e3) / max(launches, 1)
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         traffic = None
@@ -185,7 +186,7 @@ def main():
             "config": {"workload": "C2: Cornell box + 10k-tri torus knot, diffuse, 1280x720, 2 spp/frame, "
                                    "4 bounces", "width": W, "height": H, "frames_per_step": F,
                        "paths_per_step": paths_per_step, "parallelism": f"tile{world}",
-                       "gather": "RCCL gather of RGBA8 bands to rank 0 per step" if world > 1 else "none"},
+                       "gather": "RCCL gather of RGBA8 tiles to rank 0 per step" if world > 1 else "none"},
             "mrays_per_s": round(mrays, 3),
             "rays_per_path": round(rays_per_path, 4),
             "bytes_per_path": round(bytes_per_launch / max(own_paths, 1), 1),

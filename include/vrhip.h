@@ -131,6 +131,14 @@ int vrhip_render(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint3
 int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
                          uint64_t counters[8]);
 int vrhip_sync(vrhip_ctx *ctx);
+/* Path groups per pixel for vrhip_render (no reference counterpart: a launch
+ * shape knob).  A launch of k frames has 2k paths per pixel; with groups > 1
+ * they are split into that many contiguous runs on different workgroups and
+ * summed in path order afterwards, so results are unchanged.  0 (default)
+ * picks the smallest power of two that gives every CU enough workgroups
+ * (matters for small images and multi-GPU band shards); 1 disables the
+ * split.  At most 128. */
+int vrhip_set_path_split(vrhip_ctx *ctx, uint32_t groups);
 /* Frames rendered since the last clear (vRendererCuda::getFrameCount,
  * include/vRendererCuda.h:124). */
 int vrhip_frame_count(vrhip_ctx *ctx, uint32_t *frames);
@@ -143,29 +151,35 @@ int vrhip_read_depth8(vrhip_ctx *ctx, uint8_t *out_rgba8);       /* uchar4[W*H] 
 int vrhip_device_buffers(vrhip_ctx *ctx, void **accum, void **rgba8, void **depth8);
 
 /* ---- multi-GPU image-tile sharding ------------------------------------ */
-/* Render only 16-row bands b with b % n_ranks == rank (interleaved for load
- * balance).  Seeds use global pixel coordinates, so the union of the ranks'
- * bands equals the 1-GPU image bit for bit. */
+/* Render only the 16x16 tiles t (row-major over the rendered region) with
+ * t % n_ranks == rank: tiles dealt round-robin, so every rank gets the same
+ * number of tiles (+-1) spread over the whole image (sky vs mesh balance).
+ * Seeds use global pixel coordinates, so the union of the ranks' tiles equals
+ * the 1-GPU image bit for bit. */
 int vrhip_set_tiling(vrhip_ctx *ctx, uint32_t rank, uint32_t n_ranks);
-/* Host-only (no device): the rows rank `rank` of n_ranks owns for an image
- * of `height` rows, in packed order.  rows_out may be NULL to query *n_rows. */
-int vrhip_tile_rows(uint32_t height, uint32_t rank, uint32_t n_ranks, uint32_t *rows_out, uint32_t *n_rows);
-/* Number of rows this rank owns in the rendered region. */
-int vrhip_owned_rows(vrhip_ctx *ctx, uint32_t *rows);
-/* Pack this rank's owned rows (RGBA8 if what == 0, float4 accum if 1,
- * depth8 if 2) contiguously into dst (device pointer), in band order. */
-int vrhip_pack_rows(vrhip_ctx *ctx, int what, void *dst_device);
+/* Host-only (no device): linear pixel indices (y * width + x) that rank
+ * `rank` of n_ranks owns, in packed order (owned tile j holds packed pixels
+ * [256j, 256j + 256), row-major inside the tile).  pix_out may be NULL to
+ * query *n_pix. */
+int vrhip_tile_pixels(uint32_t width, uint32_t height, uint32_t rank, uint32_t n_ranks, uint32_t *pix_out,
+                      uint32_t *n_pix);
+/* Number of pixels this rank owns (256 per owned tile). */
+int vrhip_owned_pixels(vrhip_ctx *ctx, uint32_t *n_pix);
+/* Pack this rank's owned pixels (RGBA8 if what == 0, float4 accum if 1,
+ * depth8 if 2) contiguously into dst (device pointer), in packed order. */
+int vrhip_pack_tiles(vrhip_ctx *ctx, int what, void *dst_device);
 /* On the gathering rank: scatter n_ranks packed buffers from src (device;
  * rank r's buffer starts at r * stride_bytes, stride_bytes = 0 means
  * tightly packed) into this context's full image `what`. */
-int vrhip_unpack_rows(vrhip_ctx *ctx, int what, const void *src_device, uint32_t n_ranks, size_t stride_bytes);
+int vrhip_unpack_tiles(vrhip_ctx *ctx, int what, const void *src_device, uint32_t n_ranks, size_t stride_bytes);
 
 /* ---- diagnostics ------------------------------------------------------ */
 /* Kernel time of the last vrhip_render (ms, HIP events on the context stream;
  * requires vrhip_sync first). */
 int vrhip_last_kernel_ms(vrhip_ctx *ctx, float *ms);
 /* Accumulated render-kernel time (ms) and launch count since the last reset,
- * from HIP events recorded around every vrhip_render on the context stream. */
+ * from HIP events recorded around every render-kernel launch on the context
+ * stream (the split passes' finish kernel is not included). */
 int vrhip_kernel_stats(vrhip_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
 /* Raw debug slots: [0..7] the last counted render's counters; [8..13] phase
  * cycle totals (spheres, mesh traversal, hit materialisation, shading,

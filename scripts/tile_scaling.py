@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Projected strong scaling of the band sharding, measured on ONE GPU.
+
+  python scripts/tile_scaling.py [C2] [frames_per_step] [path_split, 0 = auto]
+
+For N in 1, 2, 4, 8 this renders rank 0's share of an N-way band split (rank
+0 owns the most tiles) and reports the kernel time per step, the projected
+whole-job Mpaths/s (full-image paths / rank-0 time, gather excluded) and the
+projected efficiency vs N x the 1-GPU rate.  It isolates the per-rank
+occupancy loss of strong scaling from the gather cost.
+"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+from vrenderer_pathtracer_amd import VRendererHIP, scenes  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
+F = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+SPLIT = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+sc = scenes.make_scene(cfg)
+W, H = sc["width"], sc["height"]
+paths = (W // 16) * 16 * (H // 16) * 16 * 2 * F
+r = VRendererHIP(0)
+scenes.load_into(r, sc)
+r.set_path_split(SPLIT)
+base = None
+for n in (1, 2, 4, 8):
+    r.set_tiling(0, n)
+    r.clearBuffer()
+    for i in range(2):
+        r.render(frames=F, times=[sc["time"] + i * F + k for k in range(F)])
+    r.kernel_stats(reset=True)
+    torch.cuda.synchronize()
+    steps = 6
+    t0 = time.perf_counter()
+    for i in range(steps):
+        r.render(frames=F, times=[sc["time"] + (2 + i) * F + k for k in range(F)], sync=False)
+    r.sync()
+    dt = (time.perf_counter() - t0) / steps
+    kms, launches = r.kernel_stats()
+    rate = paths / dt / 1e6
+    base = base or rate
+    print(f"{cfg} split={SPLIT} N={n}: rank-0 px {r.owned_pixels():7d}  step {dt * 1e3:8.3f} ms  kernel {kms / launches:8.3f} ms  "
+          f"projected {rate:9.1f} Mpaths/s  eff {rate / (n * base):.3f}", flush=True)
+r.cleanUp()

@@ -14,7 +14,7 @@ import pytest
 import pyoracle as po
 from vrenderer_pathtracer_amd import _native, build_flat, scenes, validate_flat
 from vrenderer_pathtracer_amd.build import LIB_PATH
-from vrenderer_pathtracer_amd.tiles import owned_rows, pack_host, unpack_host
+from vrenderer_pathtracer_amd.tiles import owned_pixels, pack_host, unpack_host
 
 _f = ctypes.POINTER(ctypes.c_float)
 
@@ -153,18 +153,26 @@ def test_random_soup_bvh_equals_brute_force(oracle):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-@pytest.mark.parametrize("H,n", [(720, 1), (720, 2), (720, 8), (1080, 8), (40, 3), (15, 2)])
-def test_tile_rows_partition(native, H, n):
-    parts = [owned_rows(H, r, n) for r in range(n)]
-    allr = np.sort(np.concatenate(parts))
-    assert np.array_equal(allr, np.arange((H // 16) * 16))
-    for r, rows in enumerate(parts):
-        assert ((rows // 16) % n == r).all()
+@pytest.mark.parametrize("W,H,n", [(1280, 720, 1), (1280, 720, 2), (1280, 720, 8), (1920, 1080, 8), (64, 40, 3),
+                                   (40, 15, 2), (48, 48, 16)])
+def test_tile_pixels_partition(native, W, H, n):
+    """Tiles dealt round-robin: a disjoint cover of the rendered region, equal counts +-1 tile."""
+    parts = [owned_pixels(W, H, r, n) for r in range(n)]
+    allp = np.sort(np.concatenate(parts))
+    wr, hr = (W // 16) * 16, (H // 16) * 16
+    expect = (np.arange(hr)[:, None] * W + np.arange(wr)[None, :]).ravel()
+    assert np.array_equal(allp, np.sort(expect))
+    tiles_x = W // 16
+    for r, pix in enumerate(parts):
+        y, x = pix // W, pix % W
+        assert (((y // 16) * tiles_x + x // 16) % n == r).all()
+    sizes = [len(p) // 256 for p in parts]
+    assert max(sizes) - min(sizes) <= 1
 
 
 def test_pack_unpack_host_roundtrip(native):
     img = np.random.default_rng(0).random((720, 64, 4)).astype(np.float32)
     packed = [pack_host(img, r, 3) for r in range(3)]
     out = np.zeros_like(img)
-    unpack_host(packed, 720, out)
+    unpack_host(packed, out)
     assert np.array_equal(out, img)

@@ -21,10 +21,12 @@ TOL_RMSE = {"hdri": 1e-3, "cornell": 2e-2}
 TOL_PIX_FRAC = 0.99
 
 
-def gpu_render(scene, frames=2, times=None, tiling=None, strict=False):
+def gpu_render(scene, frames=2, times=None, tiling=None, strict=False, split=None):
     r = VRendererHIP(0)
     scenes.load_into(r, scene)
     r.set_strict_traversal(strict)
+    if split is not None:
+        r.set_path_split(split)
     if tiling:
         r.set_tiling(*tiling)
     if times is None:
@@ -136,16 +138,72 @@ def test_grid_truncation_untouched_rows(native, oracle):
     assert np.any(ga[:32, :64, :3] != 0)
 
 
-def test_tiling_union_equals_single_gpu(native):
+@pytest.mark.parametrize("n", [3, 8])
+def test_tiling_union_equals_single_gpu(native, n):
+    from vrenderer_pathtracer_amd.tiles import owned_pixels
     sc = scenes.make_scene("C2", 160, 112)
-    full, _, _, _ = gpu_render(sc, 2)
-    n = 3
-    acc = np.zeros_like(full)
+    W, H = sc["width"], sc["height"]
+    full, rgba, depth, _ = gpu_render(sc, 2)
+    acc = np.zeros_like(full).reshape(H * W, 4)
+    seen = np.zeros(H * W, bool)
     for rank in range(n):
-        part, _, _, _ = gpu_render(sc, 2, tiling=(rank, n))
-        band = (np.arange(sc["height"]) // 16) % n == rank
-        acc[band] = part[band]
-    assert np.array_equal(acc.view(np.uint32), full.view(np.uint32))
+        part, prgba, pdepth, _ = gpu_render(sc, 2, tiling=(rank, n))
+        pix = owned_pixels(W, H, rank, n)
+        mine = np.zeros(H * W, bool)
+        mine[pix] = True
+        assert not seen[pix].any()
+        seen |= mine
+        acc[pix] = part.reshape(H * W, 4)[pix]
+        assert np.all(part.reshape(H * W, 4)[~mine] == 0)                 # nothing outside our tiles
+        assert np.array_equal(prgba.reshape(H * W, 4)[pix], rgba.reshape(H * W, 4)[pix])
+        assert np.array_equal(pdepth.reshape(H * W, 4)[pix], depth.reshape(H * W, 4)[pix])
+    assert np.array_equal(acc.view(np.uint32), full.reshape(H * W, 4).view(np.uint32))
+
+
+def test_device_pack_unpack_matches_host(native):
+    """vrhip_pack_tiles / vrhip_unpack_tiles against the host packing of the same tiles."""
+    import torch
+    from vrenderer_pathtracer_amd.tiles import WHAT_ACCUM, pack_host, max_owned_pixels
+    sc = scenes.make_scene("C1", 96, 80)
+    W, H = sc["width"], sc["height"]
+    n = 4
+    cap = max_owned_pixels(W, H, n)
+    recv = torch.zeros(n * cap * 16, dtype=torch.uint8, device="cuda")
+    full = None
+    for rank in range(n):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_tiling(rank, n)
+        r.render(frames=1, times=[sc["time"]])
+        accum = r.read_accum()
+        buf = torch.zeros(cap * 16, dtype=torch.uint8, device="cuda")
+        r.pack_tiles(WHAT_ACCUM, buf.data_ptr())
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy().view(np.float32).reshape(cap, 4)[:r.owned_pixels()]
+        assert np.array_equal(got.view(np.uint32), pack_host(accum, rank, n).view(np.uint32))
+        recv[rank * cap * 16:(rank + 1) * cap * 16] = buf
+        r.cleanUp()
+    ref, _, _, _ = gpu_render(sc, 1, [sc["time"]])
+    g = VRendererHIP(0)
+    scenes.load_into(g, sc)
+    g.unpack_tiles(WHAT_ACCUM, recv.data_ptr(), n, cap * 16)
+    g.sync()
+    full = g.read_accum()
+    g.cleanUp()
+    assert_bitexact(full, ref, sc, "unpacked accum")
+
+
+@pytest.mark.parametrize("cfg,frames", [("C2", 3), ("C3", 2), ("C4", 5), ("C1", 8)])
+def test_path_split_is_result_invariant(native, cfg, frames):
+    """Splitting a pixel's 2k paths over workgroups (vrhip_set_path_split) changes nothing."""
+    sc = scenes.make_scene(cfg, 96, 64)
+    times = [sc["time"] + 7 * i for i in range(frames)]
+    base = gpu_render(sc, frames, times, split=1)
+    for split in (2, 3, 4, 2 * frames, 0):
+        got = gpu_render(sc, frames, times, split=split)
+        assert_bitexact(got[0], base[0], sc, f"accum split={split}")
+        assert_bitexact(got[1], base[1], sc, f"rgba split={split}")
+        assert_bitexact(got[2], base[2], sc, f"depth split={split}")
 
 
 def test_multi_frame_launch_equals_frame_by_frame(native):

@@ -59,16 +59,18 @@ _SIGNATURES = {
                                           ctypes.c_int]),
     "vrhip_debug_counters": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "vrhip_sync": (ctypes.c_int, [_ctx]),
+    "vrhip_set_path_split": (ctypes.c_int, [_ctx, ctypes.c_uint32]),
     "vrhip_frame_count": (ctypes.c_int, [_ctx, _u32]),
     "vrhip_read_accum": (ctypes.c_int, [_ctx, _f]),
     "vrhip_read_rgba8": (ctypes.c_int, [_ctx, _u8]),
     "vrhip_read_depth8": (ctypes.c_int, [_ctx, _u8]),
     "vrhip_device_buffers": (ctypes.c_int, [_ctx, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
     "vrhip_set_tiling": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32]),
-    "vrhip_owned_rows": (ctypes.c_int, [_ctx, _u32]),
-    "vrhip_tile_rows": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u32, _u32]),
-    "vrhip_pack_rows": (ctypes.c_int, [_ctx, ctypes.c_int, _vp]),
-    "vrhip_unpack_rows": (ctypes.c_int, [_ctx, ctypes.c_int, _vp, ctypes.c_uint32, ctypes.c_size_t]),
+    "vrhip_owned_pixels": (ctypes.c_int, [_ctx, _u32]),
+    "vrhip_tile_pixels": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u32,
+                                         _u32]),
+    "vrhip_pack_tiles": (ctypes.c_int, [_ctx, ctypes.c_int, _vp]),
+    "vrhip_unpack_tiles": (ctypes.c_int, [_ctx, ctypes.c_int, _vp, ctypes.c_uint32, ctypes.c_size_t]),
     "vrhip_last_kernel_ms": (ctypes.c_int, [_ctx, _f]),
     "vrhip_bvh_info": (ctypes.c_int, [_ctx, _u32, _u32, _u32]),
     "vrhip_selftest_math": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _f, _f, _f, ctypes.c_size_t]),

@@ -229,6 +229,17 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
             vr4 n0, n1, nz;
             int2 ni;
             const int node = nodeAddr >> 2;
+#if defined(VR_LDS_FIRST)
+            // every lane reads LDS (uncached lanes read node 0), then the
+            // uncached lanes alone overwrite from HBM/L2
+            const bool cached = node < L.n_cached;
+            const int ln = cached ? node : 0;
+            n0 = L.nodes[3 * ln + 0];
+            n1 = L.nodes[3 * ln + 1];
+            nz = L.nodes[3 * ln + 2];
+            ni = L.idx[ln];
+            if (!cached) {
+#else
             // wave-uniform choice: a diverged wave would pay both round trips
 #ifdef VR_LANE_CACHE
             if (node < L.n_cached) {
@@ -240,6 +251,7 @@ __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& 
                 nz = L.nodes[3 * node + 2];
                 ni = L.idx[node];
             } else {
+#endif
                 const int off = nodeAddr * 16;                    // byte offset of the node
                 n0 = buf_load4(nbuf, off);
                 n1 = buf_load4(nbuf, off + 16);
@@ -660,6 +672,48 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit
     return accum;
 }
 
+// colour of the accumulated radiance after `frame` frames (PathTracer.cu:850-866)
+__device__ __forceinline__ u8x4 tonemap(vr4 io, uint32_t frame) {
+    const float coef = 1.f / (float)frame;
+    const vr4 sc = mul4s(io, coef);
+    const float inv_gamma = 1.f / 2.2f;
+    u8x4 c;
+    c.x = f2u8(pow_p(clampf(sc.x, 0.f, 1.f), inv_gamma) * 255);
+    c.y = f2u8(pow_p(clampf(sc.y, 0.f, 1.f), inv_gamma) * 255);
+    c.z = f2u8(pow_p(clampf(sc.z, 0.f, 1.f), inv_gamma) * 255);
+    c.w = 0xff;
+    return c;
+}
+
+// Split launches: sums each pixel's path results in path order (the same
+// float4 operations, in the same order, as the unsplit kernel), then writes
+// the accumulation, colour and depth.
+__global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParams p)
+{
+    const uint32_t tile = blockIdx.x, tid = threadIdx.x;
+    const int wave = (int)tid >> 6, lane = (int)tid & 63;
+    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
+    const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
+    if (x >= p.wr || y >= p.hr) return;
+    const uint32_t ind = x + y * p.W;
+    vr4 io = p.first_frame != 1u ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
+    const uint32_t n_paths = 2u * p.n_frames;
+    const vr4* src = p.paths + (size_t)tile * kBlockThreads + tid;
+    vr4 result = mk4(0.f, 0.f, 0.f, 0.f);
+    for (uint32_t q = 0; q < n_paths; ++q) {
+        result = src[(size_t)q * p.path_stride];
+        io = add4(io, mul4s(result, 1.f / 2.f));
+    }
+    const unsigned char db = f2u8((1.f - result.w) * 255);
+    u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
+    p.depth[ind] = dv;
+    p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
+    p.accum[ind] = io;
+}
+
 // render (PathTracer.cu:791-868), K frames per launch.
 #ifndef VR_MIN_WAVES_PER_SIMD
 #define VR_MIN_WAVES_PER_SIMD 4
@@ -686,18 +740,23 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
         __syncthreads();
     }
 #endif
+    // block -> (tile, path group): the 2*n_frames paths of a pixel are split
+    // into p.split contiguous groups run by different blocks (strong-scaling
+    // and tail balance); group g of tile t is block t*split + g
+    const uint32_t T = p.split;
+    const uint32_t tile = blockIdx.x / T;
+    const uint32_t g = blockIdx.x - tile * T;
     const int wave = tid >> 6, lane = tid & 63;
-    const uint32_t band_local = blockIdx.x / p.tiles_x;
-    const uint32_t tile_x = blockIdx.x - band_local * p.tiles_x;
-    const uint32_t band = p.rank + band_local * p.nranks;
+    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
     const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
-    const uint32_t y = band * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
+    const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     if (x >= p.wr || y >= p.hr) return;   // never true for a valid launch
     Cnt cnt;
     VR_T0(t_kernel);
 
     const uint32_t ind = x + y * p.W;
-    vr4 io = p.first_frame == 1 ? mk4(0.f, 0.f, 0.f, 0.f) : p.accum[ind];
     const float sx = (float)((0.25 + (double)x) / (double)p.W - 0.5);   // :842
     const float sy = (float)((0.25 + (double)y) / (double)p.H - 0.5);
     Ray cam;
@@ -707,32 +766,40 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     bool hit0 = false;
     if (!COUNT) hit0 = intersect_scene<STACK, COUNT, FEAT>(p, cam, hr0, L, cnt);
 
-    for (uint32_t f = 0; f < p.n_frames; ++f) {
-        const uint32_t frame = p.first_frame + f;
-        uint32_t s1 = x * frame;
-        uint32_t s2 = y * p.times[f];
-        unsigned char db = 0;
+    // path q = 2*f + s (frame f of the launch, sample s); the seeds of a
+    // frame's second sample are its first sample's after one hash (:620-622)
+    const uint32_t n_paths = 2u * p.n_frames;
+    const uint32_t chunk = (n_paths + T - 1u) / T;
+    const uint32_t q0 = g * chunk;
+    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
+    vr4 io = (T == 1u && p.first_frame != 1u) ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
+    uint32_t s1 = 0, s2 = 0;
+    float last_w = 0.f;
 #pragma unroll 1
-        for (int s = 0; s < 2; ++s) {
-            const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, L, cnt);
-            db = f2u8((1.f - result.w) * 255);
-            io = add4(io, mul4s(result, 1.f / 2.f));
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t f = q >> 1;
+        if ((q & 1u) == 0u || q == q0) {
+            s1 = x * (p.first_frame + f);
+            s2 = y * p.times[f];
+            if (q & 1u) (void)hash_seeds(s1, s2);
         }
-        u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
-        p.depth[ind] = dv;
-        VR_T0(t_tone);
-        const float coef = 1.f / (float)frame;
-        const vr4 sc = mul4s(io, coef);
-        const float inv_gamma = 1.f / 2.2f;
-        u8x4 c;
-        c.x = f2u8(pow_p(clampf(sc.x, 0.f, 1.f), inv_gamma) * 255);
-        c.y = f2u8(pow_p(clampf(sc.y, 0.f, 1.f), inv_gamma) * 255);
-        c.z = f2u8(pow_p(clampf(sc.z, 0.f, 1.f), inv_gamma) * 255);
-        c.w = 0xff;
-        p.rgba[ind] = c;
-        VR_T1(t_tone, 4);
+        const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, L, cnt);
+        if (T == 1u)
+            io = add4(io, mul4s(result, 1.f / 2.f));
+        else
+            p.paths[(size_t)q * p.path_stride + (size_t)tile * kBlockThreads + tid] = result;
+        last_w = result.w;
     }
+    if (T != 1u) return;   // finish_kernel accumulates the groups' results in path order
+    VR_T0(t_tone);
+    // only the launch's last frame is observable in the colour and depth
+    // surfaces (each frame of the reference overwrites them, :846-866)
+    const unsigned char db = f2u8((1.f - last_w) * 255);
+    u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
+    p.depth[ind] = dv;
+    p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
     p.accum[ind] = io;
+    VR_T1(t_tone, 4);
 #ifdef VR_TIMING
     VR_T1(t_kernel, 5);
     if (p.counters) {
@@ -768,18 +835,19 @@ __global__ void half_to_float_kernel(const uint16_t* __restrict__ src, vr4* __re
                  __half2float(__ushort_as_half(s[2])), __half2float(__ushort_as_half(s[3])));
 }
 
-// Copies this rank's 16-row bands between the full image and a packed buffer.
-__global__ void pack_rows_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                 uint32_t words_per_row, uint32_t owned_rows, uint32_t rank,
-                                 uint32_t nranks, int unpack)
+// Copies this rank's tiles between the full image and a packed buffer: owned
+// tile j (global tile rank + j*nranks) occupies packed pixels [256j, 256j+256)
+// in row-major order within the tile.
+__global__ void pack_tiles_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t wpp,
+                                  uint32_t W, uint32_t tiles_x, uint32_t rank, uint32_t nranks, int unpack)
 {
-    const uint32_t row = blockIdx.y;
-    if (row >= owned_rows) return;
-    const uint32_t band = rank + (row / 16u) * nranks;
-    const uint32_t y = band * 16u + (row % 16u);
-    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < words_per_row; w += gridDim.x * blockDim.x) {
-        const size_t full = (size_t)y * words_per_row + w;
-        const size_t packed = (size_t)row * words_per_row + w;
+    const uint32_t j = blockIdx.x;
+    const uint32_t gt = rank + j * nranks;
+    const uint32_t ty = gt / tiles_x, tx = gt - ty * tiles_x;
+    for (uint32_t w = threadIdx.x; w < 256u * wpp; w += blockDim.x) {
+        const uint32_t px = w / wpp, word = w - px * wpp;
+        const size_t full = ((size_t)(ty * 16u + px / 16u) * W + tx * 16u + px % 16u) * wpp + word;
+        const size_t packed = ((size_t)j * 256u + px) * wpp + word;
         if (unpack) dst[full] = src[packed];
         else dst[packed] = src[full];
     }
@@ -816,15 +884,15 @@ constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_S
 constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
 
 template <uint32_t FEAT>
-static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
+static void launch_spec(const RenderParams& p, uint32_t blocks, int stack_depth, hipStream_t s)
 {
 #ifndef VR_MIN_SPEC_STACK
 #define VR_MIN_SPEC_STACK 16
 #endif
     if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
-        hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+        hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
     else
-        hipLaunchKernelGGL((render_kernel<32, false, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+        hipLaunchKernelGGL((render_kernel<32, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
 }
 
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream)
@@ -833,26 +901,34 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool
     hipStream_t s = (hipStream_t)stream;
     const uint32_t need = p.flags & kFeatAll;
     auto covers = [need](uint32_t feat) { return (need & ~feat) == 0u; };
+    const uint32_t blocks = n_tiles * p.split;   // split == 1 for the counting variant
     if (count || stack_depth > 32) {
         if (count) {
-            if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, true, kFeatAll>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
-            else hipLaunchKernelGGL((render_kernel<64, true, kFeatAll>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+            if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+            else hipLaunchKernelGGL((render_kernel<64, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
         } else {
-            hipLaunchKernelGGL((render_kernel<64, false, kFeatAll>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+            hipLaunchKernelGGL((render_kernel<64, false, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
         }
     } else if (covers(kFeatCornellMesh)) {
-        launch_spec<kFeatCornellMesh>(p, n_tiles, stack_depth, s);
+        launch_spec<kFeatCornellMesh>(p, blocks, stack_depth, s);
     } else if (covers(kFeatCornellSphere)) {
-        launch_spec<kFeatCornellSphere>(p, n_tiles, stack_depth, s);
+        launch_spec<kFeatCornellSphere>(p, blocks, stack_depth, s);
     } else if (covers(kFeatHdriMesh)) {
-        launch_spec<kFeatHdriMesh>(p, n_tiles, stack_depth, s);
+        launch_spec<kFeatHdriMesh>(p, blocks, stack_depth, s);
     } else if (covers(kFeatHdriMeshTex)) {
-        launch_spec<kFeatHdriMeshTex>(p, n_tiles, stack_depth, s);
+        launch_spec<kFeatHdriMeshTex>(p, blocks, stack_depth, s);
     } else if (covers(kFeatHdriBrdfSphere)) {
-        launch_spec<kFeatHdriBrdfSphere>(p, n_tiles, stack_depth, s);
+        launch_spec<kFeatHdriBrdfSphere>(p, blocks, stack_depth, s);
     } else {
-        launch_spec<kFeatAll>(p, n_tiles, stack_depth, s);
+        launch_spec<kFeatAll>(p, blocks, stack_depth, s);
     }
+    return (int)hipGetLastError();
+}
+
+int launch_finish(const RenderParams& p, uint32_t n_tiles, void* stream)
+{
+    if (n_tiles == 0 || p.split <= 1u) return 0;
+    hipLaunchKernelGGL(finish_kernel, dim3(n_tiles), dim3(kBlockThreads), 0, (hipStream_t)stream, p);
     return (int)hipGetLastError();
 }
 
@@ -864,17 +940,12 @@ int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream)
     return (int)hipGetLastError();
 }
 
-int launch_pack_rows(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t hr,
-                     uint32_t rank, uint32_t nranks, int unpack, void* stream)
+int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,
+                      uint32_t n_owned, uint32_t rank, uint32_t nranks, int unpack, void* stream)
 {
-    const uint32_t bands = hr / 16u;
-    const uint32_t owned_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
-    const uint32_t owned_rows = owned_bands * 16u;
-    if (owned_rows == 0) return 0;
-    const uint32_t words = W * elem_bytes / 4u;
-    const unsigned bx = (words + 255) / 256 > 64 ? 64 : (words + 255) / 256;
-    hipLaunchKernelGGL(pack_rows_kernel, dim3(bx, owned_rows), dim3(256), 0, (hipStream_t)stream,
-                       (const uint32_t*)src, (uint32_t*)dst, words, owned_rows, rank, nranks, unpack);
+    if (n_owned == 0) return 0;
+    hipLaunchKernelGGL(pack_tiles_kernel, dim3(n_owned), dim3(256), 0, (hipStream_t)stream,
+                       (const uint32_t*)src, (uint32_t*)dst, elem_bytes / 4u, W, tiles_x, rank, nranks, unpack);
     return (int)hipGetLastError();
 }
 

@@ -37,8 +37,11 @@ struct RenderParams {
     float fresnel_coef, fresnel_pow;
     uint32_t flags;
     uint32_t tiles_x;                // wr / 16
-    uint32_t rank, nranks;           // interleaved 16-row band sharding
+    uint32_t rank, nranks;           // 16x16 tiles dealt round-robin: rank owns tiles rank + j*nranks
     uint32_t first_frame, n_frames;
+    uint32_t split;                  // path groups per pixel (1: a thread runs all 2*n_frames paths)
+    uint32_t path_stride;            // split > 1: owned tiles * 256 (scratch row length)
+    vr4* paths;                      // split > 1: per-path results [2*n_frames][path_stride]
     const vr4* bvh;
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
     const vr3* verts;                // 3 vertices per triangle, compact leaf order
@@ -60,9 +63,11 @@ struct RenderParams {
 
 // host-side launchers implemented in vr_kernel.hip
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream);
+// split launches only: sums the per-path results of launch_render in path order
+int launch_finish(const RenderParams& p, uint32_t n_tiles, void* stream);
 int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);
-int launch_pack_rows(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t hr,
-                     uint32_t rank, uint32_t nranks, int unpack, void* stream);
+int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,
+                      uint32_t n_owned, uint32_t rank, uint32_t nranks, int unpack, void* stream);
 int launch_selftest_math(int fn, const float* a, const float* b, float* out, size_t n, void* stream);
 
 } // namespace vr

@@ -69,8 +69,15 @@ struct vrhip_ctx {
     float* brdf = nullptr;
     // sharding
     uint32_t rank = 0, nranks = 1;
+    // path groups per pixel (0: automatic) and their result scratch
+    uint32_t path_split = 0;
+    uint32_t cu_count = 256;
+    vr4* paths = nullptr;
+    size_t paths_cap = 0;        // float4 elements
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> kev; // render-kernel start/stop pairs of the last render
+    uint32_t kev_pairs = 0;
     bool timed = false;          // ev0/ev1 hold the last render
     bool pending = false;        // last render's time not yet added to the totals
     double kernel_ms_total = 0.0;
@@ -99,11 +106,12 @@ int clear_accum(vrhip_ctx* c)
 
 uint32_t rendered_rows(const vrhip_ctx* c) { return (c->H / 16u) * 16u; }
 
-uint32_t owned_rows_of(const vrhip_ctx* c, uint32_t rank)
+// 16x16 tiles of the rendered region, dealt round-robin: rank r owns tiles
+// r, r + n, r + 2n, ... (row-major tile order)
+uint32_t owned_tiles_of(uint32_t W, uint32_t H, uint32_t rank, uint32_t n_ranks)
 {
-    const uint32_t bands = c->H / 16u;
-    const uint32_t owned = bands > rank ? (bands - rank + c->nranks - 1) / c->nranks : 0;
-    return owned * 16u;
+    const uint32_t total = (W / 16u) * (H / 16u);
+    return total > rank ? (total - rank + n_ranks - 1u) / n_ranks : 0u;
 }
 
 // Device mesh layout (see vr_kernel.hip): the reference nodes with leaf
@@ -266,6 +274,9 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(VRHIP_ERR_HIP, "hipStreamCreate failed"));
     c->stream = c->own_stream;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->cu_count = (uint32_t)cus;
     const size_t npx = (size_t)width * height;
     if (hipMalloc((void**)&c->accum, sizeof(vr4) * npx) != hipSuccess ||
         hipMalloc((void**)&c->rgba, 4 * npx) != hipSuccess ||
@@ -290,9 +301,10 @@ int vrhip_destroy(vrhip_ctx* c)
     dfree(c->accum); dfree(c->rgba); dfree(c->depth);
     dfree(c->bvh); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
-    dfree(c->counters);
+    dfree(c->counters); dfree(c->paths);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return VRHIP_OK;
@@ -441,13 +453,32 @@ static int account_pending(vrhip_ctx* c)
 {
     if (!c->pending) return VRHIP_OK;
     HIP_TRY(hipEventSynchronize(c->ev1));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    c->kernel_ms_total += ms;
+    for (uint32_t i = 0; i < c->kev_pairs; ++i) {   // render kernel only (finish passes excluded)
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->kev[2 * i], c->kev[2 * i + 1]));
+        c->kernel_ms_total += ms;
+    }
     c->launches_total += c->launches_pending;
     c->pending = false;
     c->launches_pending = 0;
     return VRHIP_OK;
+}
+
+// Path groups per pixel for a launch of n_tiles tiles x k frames.  A thread
+// runs its pixel's paths back to back, so a launch needs enough (tile, group)
+// blocks to fill every CU several times over; otherwise the few heaviest
+// tiles (mesh-covered, long bounce chains) set the launch time.  Splitting
+// the 2k paths over more blocks costs one primary ray per group and a
+// 16 B/path result round trip through HBM.
+static uint32_t choose_split(const vrhip_ctx* c, uint32_t n_tiles, uint32_t k)
+{
+    uint32_t t = c->path_split;
+    if (t == 0) {
+        const uint32_t target = c->cu_count * 64u;    // blocks: 4 resident per CU x 16 rounds (measured, C2/C3)
+        t = 1;
+        while (n_tiles * t < target && t < 2u * k) t *= 2;
+    }
+    return std::max<uint32_t>(1u, std::min<uint32_t>(t, 2u * k));
 }
 
 static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed, bool count)
@@ -486,7 +517,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
     p.brdf = c->brdf;
     p.accum = c->accum; p.rgba = c->rgba; p.depth = c->depth;
-    const uint32_t n_tiles = (owned_rows_of(c, c->rank) / 16u) * p.tiles_x;
+    const uint32_t n_tiles = owned_tiles_of(c->W, c->H, c->rank, c->nranks);
     const int stack = c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 30 ? 32 : 64;   // entries needed: depth + 1
     if (count) {
         if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
@@ -498,15 +529,41 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.counters = c->counters;   // diagnostic build: phase timers in slots 8..13
 #endif
     if ((rc = account_pending(c)) != VRHIP_OK) return rc;
+    const uint32_t k_max = std::min<uint32_t>(n_frames, (uint32_t)vr::kMaxFramesPerLaunch);
+    const uint32_t split_max = count ? 1u : choose_split(c, n_tiles, k_max);
+    p.path_stride = n_tiles * (uint32_t)vr::kBlockThreads;
+    if (split_max > 1u) {
+        const size_t need = (size_t)2 * k_max * p.path_stride;
+        if (need > c->paths_cap) {
+            dfree(c->paths);
+            c->paths_cap = 0;
+            HIP_TRY(hipMalloc((void**)&c->paths, need * sizeof(vr4)));
+            c->paths_cap = need;
+        }
+        p.paths = c->paths;
+    }
+    const uint32_t iters = (n_frames + vr::kMaxFramesPerLaunch - 1) / vr::kMaxFramesPerLaunch;
+    while (c->kev.size() < 2 * (size_t)iters) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(hipEventCreate(&e));
+        c->kev.push_back(e);
+    }
+    c->kev_pairs = 0;
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     uint32_t done = 0;
     while (done < n_frames) {
         const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
         p.first_frame = c->frame;
         p.n_frames = k;
+        p.split = std::min<uint32_t>(split_max, 2u * k);
         for (uint32_t i = 0; i < k; ++i) p.times[i] = times ? times[done + i] : time_seed;
+        HIP_TRY(hipEventRecord(c->kev[2 * c->kev_pairs], c->stream));
         int e = vr::launch_render(p, n_tiles, stack, count, c->stream);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
+        HIP_TRY(hipEventRecord(c->kev[2 * c->kev_pairs + 1], c->stream));
+        ++c->kev_pairs;
+        e = vr::launch_finish(p, n_tiles, c->stream);
+        if (e != 0) return fail(VRHIP_ERR_HIP, std::string("finish launch: ") + hipGetErrorString((hipError_t)e));
         c->frame += k;
         done += k;
         c->launches_pending += n_tiles ? 1 : 0;
@@ -603,52 +660,61 @@ int vrhip_set_tiling(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks)
     return VRHIP_OK;
 }
 
-int vrhip_tile_rows(uint32_t height, uint32_t rank, uint32_t n_ranks, uint32_t* rows_out, uint32_t* n_rows)
+int vrhip_set_path_split(vrhip_ctx* c, uint32_t groups)
 {
-    if (!n_rows || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad tiling arguments");
-    const uint32_t bands = height / 16u;
-    uint32_t n = 0;
-    for (uint32_t b = rank; b < bands; b += n_ranks)
-        for (uint32_t r = 0; r < 16u; ++r, ++n)
-            if (rows_out) rows_out[n] = b * 16u + r;
-    *n_rows = n;
+    if (!c || groups > 2u * vr::kMaxFramesPerLaunch) return fail(VRHIP_ERR_INVALID, "bad path split");
+    c->path_split = groups;
     return VRHIP_OK;
 }
 
-int vrhip_owned_rows(vrhip_ctx* c, uint32_t* rows)
+int vrhip_tile_pixels(uint32_t width, uint32_t height, uint32_t rank, uint32_t n_ranks, uint32_t* pix_out,
+                      uint32_t* n_pix)
 {
-    if (!c || !rows) return fail(VRHIP_ERR_INVALID, "null argument");
-    *rows = owned_rows_of(c, c->rank);
+    if (!n_pix || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad tiling arguments");
+    const uint32_t tiles_x = width / 16u, n_owned = owned_tiles_of(width, height, rank, n_ranks);
+    *n_pix = n_owned * 256u;
+    if (pix_out) {
+        for (uint32_t j = 0; j < n_owned; ++j) {
+            const uint32_t gt = rank + j * n_ranks, ty = gt / tiles_x, tx = gt - ty * tiles_x;
+            for (uint32_t px = 0; px < 256u; ++px)
+                pix_out[j * 256u + px] = (ty * 16u + px / 16u) * width + tx * 16u + px % 16u;
+        }
+    }
+    return VRHIP_OK;
+}
+
+int vrhip_owned_pixels(vrhip_ctx* c, uint32_t* n_pix)
+{
+    if (!c || !n_pix) return fail(VRHIP_ERR_INVALID, "null argument");
+    *n_pix = owned_tiles_of(c->W, c->H, c->rank, c->nranks) * 256u;
     return VRHIP_OK;
 }
 
 static int elem_size(int what) { return what == 1 ? 16 : 4; }
 static const void* buf_of(vrhip_ctx* c, int what) { return what == 1 ? (const void*)c->accum : what == 2 ? (const void*)c->depth : (const void*)c->rgba; }
 
-int vrhip_pack_rows(vrhip_ctx* c, int what, void* dst)
+int vrhip_pack_tiles(vrhip_ctx* c, int what, void* dst)
 {
     if (!c || !dst || what < 0 || what > 2) return fail(VRHIP_ERR_INVALID, "bad pack arguments");
     int rc = set_device(c); if (rc) return rc;
-    int e = vr::launch_pack_rows(buf_of(c, what), dst, (uint32_t)elem_size(what), c->W, rendered_rows(c),
-                                 c->rank, c->nranks, 0, c->stream);
+    int e = vr::launch_pack_tiles(buf_of(c, what), dst, (uint32_t)elem_size(what), c->W, c->W / 16u,
+                                  owned_tiles_of(c->W, c->H, c->rank, c->nranks), c->rank, c->nranks, 0, c->stream);
     if (e) return fail(VRHIP_ERR_HIP, "pack launch failed");
     return VRHIP_OK;
 }
 
-int vrhip_unpack_rows(vrhip_ctx* c, int what, const void* src, uint32_t n_ranks, size_t stride_bytes)
+int vrhip_unpack_tiles(vrhip_ctx* c, int what, const void* src, uint32_t n_ranks, size_t stride_bytes)
 {
     if (!c || !src || what < 0 || what > 2 || n_ranks == 0) return fail(VRHIP_ERR_INVALID, "bad unpack arguments");
     int rc = set_device(c); if (rc) return rc;
-    const uint32_t saved_n = c->nranks;
-    c->nranks = n_ranks;
     const char* s = (const char*)src;
     for (uint32_t r = 0; r < n_ranks; ++r) {
-        int e = vr::launch_pack_rows(s, const_cast<void*>(buf_of(c, what)), (uint32_t)elem_size(what), c->W,
-                                     rendered_rows(c), r, n_ranks, 1, c->stream);
-        if (e) { c->nranks = saved_n; return fail(VRHIP_ERR_HIP, "unpack launch failed"); }
-        s += stride_bytes ? stride_bytes : (size_t)owned_rows_of(c, r) * c->W * elem_size(what);
+        const uint32_t n_owned = owned_tiles_of(c->W, c->H, r, n_ranks);
+        int e = vr::launch_pack_tiles(s, const_cast<void*>(buf_of(c, what)), (uint32_t)elem_size(what), c->W,
+                                      c->W / 16u, n_owned, r, n_ranks, 1, c->stream);
+        if (e) return fail(VRHIP_ERR_HIP, "unpack launch failed");
+        s += stride_bytes ? stride_bytes : (size_t)n_owned * 256u * elem_size(what);
     }
-    c->nranks = saved_n;
     return VRHIP_OK;
 }
 

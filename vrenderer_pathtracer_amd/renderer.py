@@ -279,17 +279,22 @@ class VRendererHIP:
     def set_tiling(self, rank: int, n_ranks: int) -> None:
         check(self._lib.vrhip_set_tiling(self._need_ctx(), rank, n_ranks), "vrhip_set_tiling")
 
-    def owned_rows(self) -> int:
+    def set_path_split(self, groups: int) -> None:
+        """Path groups per pixel per launch (0 = automatic, 1 = off); results are unchanged."""
+        check(self._lib.vrhip_set_path_split(self._need_ctx(), groups), "vrhip_set_path_split")
+
+    def owned_pixels(self) -> int:
+        """Pixels this rank renders (256 per owned 16x16 tile)."""
         n = ctypes.c_uint32(0)
-        check(self._lib.vrhip_owned_rows(self._need_ctx(), ctypes.byref(n)), "vrhip_owned_rows")
+        check(self._lib.vrhip_owned_pixels(self._need_ctx(), ctypes.byref(n)), "vrhip_owned_pixels")
         return n.value
 
-    def pack_rows(self, what: int, dst_ptr: int) -> None:
-        check(self._lib.vrhip_pack_rows(self._need_ctx(), what, ctypes.c_void_p(dst_ptr)), "vrhip_pack_rows")
+    def pack_tiles(self, what: int, dst_ptr: int) -> None:
+        check(self._lib.vrhip_pack_tiles(self._need_ctx(), what, ctypes.c_void_p(dst_ptr)), "vrhip_pack_tiles")
 
-    def unpack_rows(self, what: int, src_ptr: int, n_ranks: int, stride_bytes: int = 0) -> None:
-        check(self._lib.vrhip_unpack_rows(self._need_ctx(), what, ctypes.c_void_p(src_ptr), n_ranks, stride_bytes),
-              "vrhip_unpack_rows")
+    def unpack_tiles(self, what: int, src_ptr: int, n_ranks: int, stride_bytes: int = 0) -> None:
+        check(self._lib.vrhip_unpack_tiles(self._need_ctx(), what, ctypes.c_void_p(src_ptr), n_ranks, stride_bytes),
+              "vrhip_unpack_tiles")
 
     def render_counted(self, frames: int = 1, times=None, time_seed=None) -> dict:
         """Render through the counting kernel variant; returns the event counts."""

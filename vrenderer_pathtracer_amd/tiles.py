@@ -3,12 +3,13 @@
 The reference is single-GPU; its RNG seeds depend only on global pixel
 coordinates, frame and time (cuda/src/PathTracer.cu:817-818), so any
 partition of the pixels renders the same image bit for bit.  Partition:
-16-row bands (the reference's block height, PathTracer.cu:887) dealt
-round-robin to ranks for load balance (sky vs mesh rows).  Each rank keeps its
-own float4 accumulation resident; after every accumulation step the ranks'
-RGBA8 bands (or float4 accumulation, for parity read-out) are gathered to
-rank 0 with ONE collective (torch.distributed "nccl" = RCCL over xGMI, or gloo
-on CPU) and scattered back into band order on the device.
+16x16 tiles (the reference's block, PathTracer.cu:887) dealt round-robin to
+ranks in row-major tile order, so ranks own equal tile counts (+-1) spread
+over the whole image (sky vs mesh load balance).  Each rank keeps its own
+float4 accumulation resident; after every accumulation step the ranks' RGBA8
+tiles (or float4 accumulation, for parity read-out) are gathered to rank 0
+with ONE collective (torch.distributed "nccl" = RCCL over xGMI, or gloo on
+CPU) and scattered back into image order on the device.
 """
 from __future__ import annotations
 
@@ -23,37 +24,44 @@ WHAT_RGBA8, WHAT_ACCUM, WHAT_DEPTH8 = 0, 1, 2
 _ELEM_BYTES = {WHAT_RGBA8: 4, WHAT_ACCUM: 16, WHAT_DEPTH8: 4}
 
 
-def owned_rows(height: int, rank: int, n_ranks: int) -> np.ndarray:
-    """Rows of the rendered region owned by `rank`, in packed order (C ABI vrhip_tile_rows)."""
+def owned_pixels(width: int, height: int, rank: int, n_ranks: int) -> np.ndarray:
+    """Linear pixel indices (y*W + x) owned by `rank`, in packed order (C ABI vrhip_tile_pixels)."""
     L = _native.lib()
     n = ctypes.c_uint32(0)
-    check(L.vrhip_tile_rows(height, rank, n_ranks, None, ctypes.byref(n)), "vrhip_tile_rows")
+    check(L.vrhip_tile_pixels(width, height, rank, n_ranks, None, ctypes.byref(n)), "vrhip_tile_pixels")
     out = np.zeros(n.value, np.uint32)
-    check(L.vrhip_tile_rows(height, rank, n_ranks, out.ctypes.data_as(_native._u32), ctypes.byref(n)),
-          "vrhip_tile_rows")
+    check(L.vrhip_tile_pixels(width, height, rank, n_ranks, out.ctypes.data_as(_native._u32), ctypes.byref(n)),
+          "vrhip_tile_pixels")
     return out
 
 
-def max_owned_rows(height: int, n_ranks: int) -> int:
-    return ((height // 16 + n_ranks - 1) // n_ranks) * 16
+def max_owned_pixels(width: int, height: int, n_ranks: int) -> int:
+    tiles = (width // 16) * (height // 16)
+    return ((tiles + n_ranks - 1) // n_ranks) * 256
 
 
 def pack_host(image: np.ndarray, rank: int, n_ranks: int) -> np.ndarray:
-    """Host-side packing of a rank's bands (the device does this with vrhip_pack_rows)."""
-    return np.ascontiguousarray(image[owned_rows(image.shape[0], rank, n_ranks)])
+    """Host-side packing of a rank's tiles (the device does this with vrhip_pack_tiles).
+    image: [H, W, ...] -> [n_owned_pixels, ...]."""
+    H, W = image.shape[:2]
+    flat = image.reshape(H * W, *image.shape[2:])
+    return np.ascontiguousarray(flat[owned_pixels(W, H, rank, n_ranks)])
 
 
-def unpack_host(packed: list, height: int, out: np.ndarray) -> np.ndarray:
-    """Scatter per-rank packed bands back into image order (device: vrhip_unpack_rows)."""
+def unpack_host(packed: list, out: np.ndarray) -> np.ndarray:
+    """Scatter per-rank packed pixels back into image order (device: vrhip_unpack_tiles).
+    out: [H, W, ...] image, updated in place."""
     n = len(packed)
+    H, W = out.shape[:2]
+    flat = out.reshape(H * W, *out.shape[2:])
     for r, buf in enumerate(packed):
-        rows = owned_rows(height, r, n)
-        out[rows] = buf[:len(rows)]
+        pix = owned_pixels(W, H, r, n)
+        flat[pix] = buf[:len(pix)]
     return out
 
 
-class BandGather:
-    """Per-step gather of every rank's bands to rank 0 with one collective.
+class TileGather:
+    """Per-step gather of every rank's tiles to rank 0 with one collective.
 
     renderer: VRendererHIP with set_tiling(rank, world) applied; torch tensors
     hold the send/receive buffers on the renderer's device so the collective
@@ -64,7 +72,7 @@ class BandGather:
         import torch
         self.r, self.rank, self.world, self.what = renderer, rank, world, what
         H, W = renderer.height, renderer.width
-        self.stride = max_owned_rows(H, world) * W * _ELEM_BYTES[what]
+        self.stride = max_owned_pixels(W, H, world) * _ELEM_BYTES[what]
         self.send = torch.empty(self.stride, dtype=torch.uint8, device=device)
         self.recv = None
         if rank == 0 and world > 1:
@@ -75,7 +83,7 @@ class BandGather:
         import torch.distributed as dist
         if self.world == 1:
             return
-        self.r.pack_rows(self.what, self.send.data_ptr())
+        self.r.pack_tiles(self.what, self.send.data_ptr())
         dist.gather(self.send, self.views if self.rank == 0 else None, dst=0)
         if self.rank == 0:
-            self.r.unpack_rows(self.what, self.recv.data_ptr(), self.world, self.stride)
+            self.r.unpack_tiles(self.what, self.recv.data_ptr(), self.world, self.stride)
