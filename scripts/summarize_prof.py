@@ -53,7 +53,8 @@ def main():
         traffic = int((2 * fetch[0] + write[0]) * 1024)
         json.dump({"hbm_bytes_per_launch": traffic, "fetch_size_kib": fetch[0], "write_size_kib": write[0],
                    "source": f"profiles/{name}_pmc.json", "note": "2*FETCH_SIZE+WRITE_SIZE (KiB->B) per render "
-                   "launch (8 frames of C2 1280x720); FETCH doubling per MI355X_MICROARCH.md HBM section"},
+                   "launch of bench.py's C2 step; FETCH doubling per MI355X_MICROARCH.md HBM section; WRITE is "
+                   "dominated by the split launch's 16 B/path result scratch"},
                   open(os.path.join(prof, "traffic_c2.json"), "w"), indent=1)
     bench = ""
     blog = os.path.join(src, "bench.log")
@@ -61,8 +62,9 @@ def main():
         lines = [l for l in open(blog) if l.startswith("{")]
         bench = lines[-1].strip() if lines else ""
     with open(os.path.join(prof, f"{name}_summary.md"), "w") as f:
+        fps = json.loads(bench)["config"].get("frames_per_step", "?") if bench else "?"
         f.write(f"# Profile {name}\n\nSource: `scripts/gpu_round.sh` on one MI355X, bench.py C2 (1280x720, "
-                "8 frames per launch).\n\n## rocprofv3 --kernel-trace --stats\n\n| kernel | calls | avg ms |\n|---|---|---|\n")
+                f"{fps} frames per launch).\n\n## rocprofv3 --kernel-trace --stats\n\n| kernel | calls | avg ms |\n|---|---|---|\n")
         for r in rows:
             f.write(f"| `{r['Name'][:70]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} |\n")
         f.write("\n## PMC (render kernel, per dispatch)\n\n")
@@ -79,7 +81,7 @@ def main():
                     "(FETCH doubling is calibrated for wide streams only; this kernel's reads are L2-resident gathers)\n")
         if bench:
             f.write(f"\n## bench.py line\n\n```\n{bench}\n```\n")
-    print(open(os.path.join(prof, f"{name}_summary.md")).read())
+    print(f"wrote profiles/{name}_summary.md")
 
 
 if __name__ == "__main__":

@@ -113,12 +113,24 @@ struct HitRec {
 // Per-lane event counts for the counting variant (algorithmic bytes).
 struct Cnt {
     uint32_t rays = 0, nodes = 0, slots = 0, tris = 0, attr = 0, tex = 0, hdr = 0, brdf = 0;
-#ifdef VR_TIMING
-    // diagnostic build only: per-lane s_memtime cycles in spheres, mesh
-    // traversal, hit materialisation, shading, tonemap, whole kernel
+#if defined(VR_TIMING) || defined(VR_LANESTATS)
+    // diagnostic builds only.  VR_TIMING: per-lane s_memtime cycles in
+    // spheres, mesh traversal, hit materialisation, shading, tonemap, whole
+    // kernel.  VR_LANESTATS: active lanes and wave iterations of the node
+    // loop, the triangle loop and the shading block (SIMD utilisation).
     uint64_t tm[6] = { 0, 0, 0, 0, 0, 0 };
 #endif
 };
+#ifdef VR_LANESTATS
+#define VR_LANE(sl, si)                                                              \
+    do {                                                                             \
+        const unsigned long long m_ = __ballot(1);                                   \
+        cnt.tm[sl] += 1;                                                             \
+        if ((int)__lane_id() == __ffsll((long long)m_) - 1) cnt.tm[si] += 1;         \
+    } while (0)
+#else
+#define VR_LANE(sl, si) (void)0
+#endif
 #ifdef VR_TIMING
 #define VR_T0(name) const uint64_t name = __builtin_amdgcn_s_memtime()
 #define VR_T1(name, slot) cnt.tm[slot] += __builtin_amdgcn_s_memtime() - name
@@ -196,160 +208,216 @@ struct Lds {
     int n_cached;             // nodes [0, n_cached) are read from LDS
 };
 
-template <int STACK, bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
+// CudaTracerLib-style while-while traversal (PathTracer.cu:276-463), split
+// into init / one outer iteration / finish so a wave can pause it between
+// outer iterations (render_wave_kernel) without changing any lane's sequence
+// of node visits and triangle tests.
+constexpr int kSentinel = 0x76543210;
+struct Trav {
+    float ivx, ivy, ivz, odx, ody, odz;
+    float t, tcull, bu, bv;
+    int best, sp, nodeAddr;
+    int k, kend;              // leaf in progress (trav_step only)
+};
+
+template <uint32_t FEAT>
+__device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, float t0, Trav& tr, const Lds& L)
 {
-    int* stk = L.stk;
-    const __amdgpu_buffer_rsrc_t nbuf = buf_rsrc(p.bvh, p.n_nodes * 64u);
-    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, p.n_tris * 36u);
-    // CudaTracerLib-style while-while traversal (PathTracer.cu:276-463)
-    const int Sentinel = 0x76543210;
-    int sp = 0;
-    stk[0] = Sentinel;
-    int leafAddr = 0;
-    int nodeAddr = 0;
-    const float ivx = 1.f / (__builtin_fabsf(r.d.x) > VR_EPS ? r.d.x : VR_EPS);
-    const float ivy = 1.f / (__builtin_fabsf(r.d.y) > VR_EPS ? r.d.y : VR_EPS);
-    const float ivz = 1.f / (__builtin_fabsf(r.d.z) > VR_EPS ? r.d.z : VR_EPS);
-    const float odx = r.o.x * ivx, ody = r.o.y * ivy, odz = r.o.z * ivz;
-    float t = hr.t;
+    tr.sp = 0;
+    L.stk[0] = kSentinel;
+    tr.nodeAddr = 0;
+    tr.ivx = 1.f / (__builtin_fabsf(r.d.x) > VR_EPS ? r.d.x : VR_EPS);
+    tr.ivy = 1.f / (__builtin_fabsf(r.d.y) > VR_EPS ? r.d.y : VR_EPS);
+    tr.ivz = 1.f / (__builtin_fabsf(r.d.z) > VR_EPS ? r.d.z : VR_EPS);
+    tr.odx = r.o.x * tr.ivx; tr.ody = r.o.y * tr.ivy; tr.odz = r.o.z * tr.ivz;
+    tr.t = t0;
     // t-culling: a child whose slab entry lies beyond the closest hit so far
     // (times a 2^-10 safety margin) cannot hold a closer triangle.  The
     // reference visits every pierced box (span end clamped to 1e20,
     // :316,322); F_STRICT restores that exactly.
-    const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
-    const float kCull = 1.0009765625f;
-    float tcull = strict ? __builtin_inff() : t * kCull;
-    int best = -1;
-    float bu = 0.f, bv = 0.f;
+    tr.tcull = HAS(F_STRICT) ? __builtin_inff() : t0 * 1.0009765625f;
+    tr.best = -1;
+    tr.bu = tr.bv = 0.f;
+    tr.k = tr.kend = 0;
+}
 
-    while (nodeAddr != Sentinel) {
-        while ((unsigned)nodeAddr < (unsigned)Sentinel) {
-            if (COUNT) cnt.nodes++;
-            vr4 n0, n1, nz;
-            int2 ni;
-            const int node = nodeAddr >> 2;
-#if defined(VR_LDS_FIRST)
-            // every lane reads LDS (uncached lanes read node 0), then the
-            // uncached lanes alone overwrite from HBM/L2
-            const bool cached = node < L.n_cached;
-            const int ln = cached ? node : 0;
-            n0 = L.nodes[3 * ln + 0];
-            n1 = L.nodes[3 * ln + 1];
-            nz = L.nodes[3 * ln + 2];
-            ni = L.idx[ln];
-            if (!cached) {
-#else
-            // wave-uniform choice: a diverged wave would pay both round trips
-#ifdef VR_LANE_CACHE
-            if (node < L.n_cached) {
-#else
-            if (__ballot(node >= L.n_cached) == 0ull) {
-#endif
-                n0 = L.nodes[3 * node + 0];
-                n1 = L.nodes[3 * node + 1];
-                nz = L.nodes[3 * node + 2];
-                ni = L.idx[node];
-            } else {
-#endif
-                const int off = nodeAddr * 16;                    // byte offset of the node
-                n0 = buf_load4(nbuf, off);
-                n1 = buf_load4(nbuf, off + 16);
-                nz = buf_load4(nbuf, off + 32);
-                ni = buf_load2i(nbuf, off + 48);                  // 8 of the row's 16 bytes are used
-            }
-            const int idx0 = ni.x, idx1 = ni.y;
-            // slab distances n*inv - o*inv (:307-322); the culled mode lets
-            // them contract to one v_fma each (more accurate)
-            auto slab = [&](float n, float iv, float od) {
-                return strict ? (n * iv - od) : __builtin_fmaf(n, iv, -od);
-            };
-            const float c0lox = slab(n0.x, ivx, odx);
-            const float c0hix = slab(n0.y, ivx, odx);
-            const float c0loy = slab(n0.z, ivy, ody);
-            const float c0hiy = slab(n0.w, ivy, ody);
-            const float c0loz = slab(nz.x, ivz, odz);
-            const float c0hiz = slab(nz.y, ivz, odz);
-            const float c1loz = slab(nz.z, ivz, odz);
-            const float c1hiz = slab(nz.w, ivz, odz);
-            const float c0min = span_begin(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, 0.0f);
-            const float c0max = span_end(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, 1e20f);
-            const float c1lox = slab(n1.x, ivx, odx);
-            const float c1hix = slab(n1.y, ivx, odx);
-            const float c1loy = slab(n1.z, ivy, ody);
-            const float c1hiy = slab(n1.w, ivy, ody);
-            const float c1min = span_begin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 0.0f);
-            const float c1max = span_end(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 1e20f);
-            // keep the child-index load in the same round trip as the bounds
-            asm volatile("" ::"v"(idx0), "v"(idx1));
-            const bool swp = (c1min < c0min);
-            const bool tc0 = (c0max >= c0min) && (c0min <= tcull);
-            const bool tc1 = (c1max >= c1min) && (c1min <= tcull);
-            // branch-free push/pop: near child next, far child pushed when both
-            // are hit, pop when neither is (same order as :324-343)
-            const bool both = tc0 && tc1;
-            const bool none = !tc0 && !tc1;
-            const int top = stk[sp * kBlockThreads];
-            const int nearc = (both && swp) ? idx1 : (tc0 ? idx0 : idx1);
-            const int farc = swp ? idx0 : idx1;
-            if (both) stk[(sp + 1) * kBlockThreads] = farc;
-            sp += both ? 1 : (none ? -1 : 0);
-            nodeAddr = none ? top : nearc;
-            if (nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
-                leafAddr = nodeAddr;
-                nodeAddr = stk[sp * kBlockThreads];
-                --sp;
-            }
-            if (__ballot(leafAddr >= 0) == 0ull) break;          // every lane holds a leaf
+// One outer iteration: the inner node loop until this lane holds a leaf and
+// the wave agrees (ballot), then the leaf loop.  Precondition: tr.nodeAddr is
+// an inner node (not kSentinel).
+// One inner-node visit (:295-343): fetch (LDS copy or L2/HBM), two slab
+// tests, near child next, far child pushed when both are entered, pop when
+// neither is.  Leaves in tr.nodeAddr are left to the caller.
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
+{
+    int* stk = L.stk;
+    const __amdgpu_buffer_rsrc_t nbuf = buf_rsrc(p.bvh, p.n_nodes * 64u);
+    const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
+    if (COUNT) cnt.nodes++;
+    VR_LANE(0, 1);
+    vr4 n0, n1, nz;
+    int2 ni;
+    const int node = tr.nodeAddr >> 2;
+    // wave-uniform choice: a diverged wave would pay both round trips
+    if (__ballot(node >= L.n_cached) == 0ull) {
+        n0 = L.nodes[3 * node + 0];
+        n1 = L.nodes[3 * node + 1];
+        nz = L.nodes[3 * node + 2];
+        ni = L.idx[node];
+    } else {
+        const int off = tr.nodeAddr * 16;                     // byte offset of the node
+        n0 = buf_load4(nbuf, off);
+        n1 = buf_load4(nbuf, off + 16);
+        nz = buf_load4(nbuf, off + 32);
+        ni = buf_load2i(nbuf, off + 48);                      // 8 of the row's 16 bytes are used
+    }
+    const int idx0 = ni.x, idx1 = ni.y;
+    // slab distances n*inv - o*inv (:307-322); the culled mode lets
+    // them contract to one v_fma each (more accurate)
+    auto slab = [&](float n, float iv, float od) {
+        return strict ? (n * iv - od) : __builtin_fmaf(n, iv, -od);
+    };
+    const float c0lox = slab(n0.x, tr.ivx, tr.odx);
+    const float c0hix = slab(n0.y, tr.ivx, tr.odx);
+    const float c0loy = slab(n0.z, tr.ivy, tr.ody);
+    const float c0hiy = slab(n0.w, tr.ivy, tr.ody);
+    const float c0loz = slab(nz.x, tr.ivz, tr.odz);
+    const float c0hiz = slab(nz.y, tr.ivz, tr.odz);
+    const float c1loz = slab(nz.z, tr.ivz, tr.odz);
+    const float c1hiz = slab(nz.w, tr.ivz, tr.odz);
+    const float c0min = span_begin(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, 0.0f);
+    const float c0max = span_end(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, 1e20f);
+    const float c1lox = slab(n1.x, tr.ivx, tr.odx);
+    const float c1hix = slab(n1.y, tr.ivx, tr.odx);
+    const float c1loy = slab(n1.z, tr.ivy, tr.ody);
+    const float c1hiy = slab(n1.w, tr.ivy, tr.ody);
+    const float c1min = span_begin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 0.0f);
+    const float c1max = span_end(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 1e20f);
+    // keep the child-index load in the same round trip as the bounds
+    asm volatile("" ::"v"(idx0), "v"(idx1));
+    const bool swp = (c1min < c0min);
+    const bool tc0 = (c0max >= c0min) && (c0min <= tr.tcull);
+    const bool tc1 = (c1max >= c1min) && (c1min <= tr.tcull);
+    // branch-free push/pop: near child next, far child pushed when both
+    // are hit, pop when neither is (same order as :324-343)
+    const bool both = tc0 && tc1;
+    const bool none = !tc0 && !tc1;
+    const int top = stk[tr.sp * kBlockThreads];
+    const int nearc = (both && swp) ? idx1 : (tc0 ? idx0 : idx1);
+    const int farc = swp ? idx0 : idx1;
+    if (both) stk[(tr.sp + 1) * kBlockThreads] = farc;
+    tr.sp += both ? 1 : (none ? -1 : 0);
+    tr.nodeAddr = none ? top : nearc;
+}
+
+// intersectTriangle (RayIntersection.cuh:54-111) for compact triangle k and
+// the closest-hit update (:379-386).  Evaluated branch-free: every early
+// return of the reference becomes a term of the final predicate (the values
+// computed for a surviving triangle are the same operations in the same order).
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Trav& tr, int k, Cnt& cnt)
+{
+    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, p.n_tris * 36u);
+    const bool strict = HAS(F_STRICT);
+    if (COUNT) cnt.tris++;
+    VR_LANE(2, 3);
+    const int toff = k * 36;
+    const vr3 a0 = buf_load3(tbuf, toff), a1 = buf_load3(tbuf, toff + 12), a2 = buf_load3(tbuf, toff + 24);
+    asm volatile("" ::"v"(a0.x), "v"(a1.x), "v"(a2.x));   // three dwordx3 loads, one trip
+    const vr4 v0 = mk4(a0.x, a0.y, a0.z, 0.f);
+    const vr4 v1 = mk4(a1.x, a1.y, a1.z, 0.f);
+    const vr4 v2 = mk4(a2.x, a2.y, a2.z, 0.f);
+    const vr4 e1 = sub4(v1, v0), e2 = sub4(v2, v0);
+    const vr4 pv = cross4(r.d, e2);
+    const float det = dot4(e1, pv);
+    const float inv_det = 1.f / det;
+    const vr4 tv = sub4(r.o, v0);
+    const float u = dot4(tv, pv) * inv_det;
+    const vr4 q = cross4(tv, e1);
+    const float v = dot4(r.d, q) * inv_det;
+    const float dist = dot4(e2, q) * inv_det;
+    const bool ok = !(det > -VR_EPS && det < VR_EPS) && !(u < 0.f || u > 1.f) &&
+                    !(v < 0.f || u + v > 1.f);
+    if (ok && dist > VR_EPS && dist < tr.t) {
+        tr.t = dist; tr.best = 3 * k; tr.bu = u; tr.bv = v;
+        tr.tcull = strict ? tr.tcull : tr.t * 1.0009765625f;
+    }
+}
+
+// One outer iteration of the while-while loop: the inner node loop until
+// this lane holds a leaf and the wave agrees (ballot, :353-363), with one
+// leaf postponed (:345-351), then the leaf loop.  Precondition: tr.nodeAddr
+// is an inner node (not kSentinel).
+template <int STACK, bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
+{
+    int* stk = L.stk;
+    int leafAddr = 0;
+    while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
+        node_step<COUNT, FEAT>(p, r, tr, L, cnt);
+        if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
+            leafAddr = tr.nodeAddr;
+            tr.nodeAddr = stk[tr.sp * kBlockThreads];
+            --tr.sp;
         }
-        while (leafAddr < 0) {
-            const int lv = ~leafAddr;
-            const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
-            for (int k = lv >> kLeafCountBits; k < kend; ++k) {
-                const int triAddr = 3 * k;
-                if (COUNT) cnt.tris++;
-                const int toff = k * 36;
-                const vr3 a0 = buf_load3(tbuf, toff), a1 = buf_load3(tbuf, toff + 12), a2 = buf_load3(tbuf, toff + 24);
-                asm volatile("" ::"v"(a0.x), "v"(a1.x), "v"(a2.x));   // three dwordx3 loads, one trip
-                const vr4 v0 = mk4(a0.x, a0.y, a0.z, 0.f);
-                const vr4 v1 = mk4(a1.x, a1.y, a1.z, 0.f);
-                const vr4 v2 = mk4(a2.x, a2.y, a2.z, 0.f);
-                // intersectTriangle, RayIntersection.cuh:54-111, evaluated
-                // branch-free: every early return of the reference becomes a
-                // term of the final predicate (the values computed for a
-                // surviving triangle are the same operations in the same order)
-                const vr4 e1 = sub4(v1, v0), e2 = sub4(v2, v0);
-                const vr4 pv = cross4(r.d, e2);
-                const float det = dot4(e1, pv);
-                const float inv_det = 1.f / det;
-                const vr4 tv = sub4(r.o, v0);
-                const float u = dot4(tv, pv) * inv_det;
-                const vr4 q = cross4(tv, e1);
-                const float v = dot4(r.d, q) * inv_det;
-                const float dist = dot4(e2, q) * inv_det;
-                const bool ok = !(det > -VR_EPS && det < VR_EPS) && !(u < 0.f || u > 1.f) &&
-                                !(v < 0.f || u + v > 1.f);
-                if (ok && dist > VR_EPS && dist < t) {
-                    t = dist; best = triAddr; bu = u; bv = v;
-                    tcull = strict ? tcull : t * kCull;
-                }
-            }
-            leafAddr = nodeAddr;
-            if (nodeAddr < 0) {
-                nodeAddr = stk[sp * kBlockThreads];
-                --sp;
-            }
+        if (__ballot(leafAddr >= 0) == 0ull) break;          // every lane holds a leaf
+    }
+    while (leafAddr < 0) {
+        const int lv = ~leafAddr;
+        const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
+        for (int k = lv >> kLeafCountBits; k < kend; ++k) tri_test<COUNT, FEAT>(p, r, tr, k, cnt);
+        leafAddr = tr.nodeAddr;
+        if (tr.nodeAddr < 0) {
+            tr.nodeAddr = stk[tr.sp * kBlockThreads];
+            --tr.sp;
         }
     }
-    if (best >= 0) { hr.t = t; hr.kind = HK_MESH; hr.idx = best; hr.bu = bu; hr.bv = bv; }
+}
+
+// If-if alternative: one unit of work per call -- the next triangle of the
+// leaf in progress, else one node visit; a leaf reached is started at once
+// (the leaves, and the triangles within each, are tested in the same order
+// as by trav_iter).  Lanes stay busy with whichever kind of step they need.
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void trav_step(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
+{
+    if (tr.k < tr.kend) {
+        tri_test<COUNT, FEAT>(p, r, tr, tr.k, cnt);
+        ++tr.k;
+    } else {
+        node_step<COUNT, FEAT>(p, r, tr, L, cnt);
+    }
+    if (tr.k >= tr.kend && tr.nodeAddr < 0) {                // start the leaf, resume at the stack top
+        const int lv = ~tr.nodeAddr;
+        tr.k = lv >> kLeafCountBits;
+        tr.kend = tr.k + (lv & ((1 << kLeafCountBits) - 1));
+        tr.nodeAddr = L.stk[tr.sp * kBlockThreads];
+        --tr.sp;
+    }
+}
+
+__device__ __forceinline__ void trav_finish(const Trav& tr, HitRec& hr)
+{
+    if (tr.best >= 0) { hr.t = tr.t; hr.kind = HK_MESH; hr.idx = tr.best; hr.bu = tr.bu; hr.bv = tr.bv; }
+}
+
+template <int STACK, bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
+{
+    Trav tr;
+    trav_init<FEAT>(p, r, hr.t, tr, L);
+    while (tr.nodeAddr != kSentinel) trav_iter<STACK, COUNT, FEAT>(p, r, tr, L, cnt);
+    trav_finish(tr, hr);
 }
 
 // intersectScene (PathTracer.cu:136-468): closest hit, attributes deferred.
-template <int STACK, bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
+// intersectScene (PathTracer.cu:136-468), sphere part: Cornell walls and
+// light, the two small spheres, the example sphere.  Returns true when the
+// mesh must still be traversed (kMeshInitialised and no example sphere).
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool intersect_spheres(const RenderParams& p, const Ray& r, HitRec& hr, Cnt& cnt)
 {
     if (COUNT) cnt.rays++;
-    VR_T0(t_sph);
     hr.t = 1e20f; hr.kind = HK_NONE; hr.idx = 0; hr.bu = hr.bv = 0.f; hr.su = hr.sv = 0.f;
     if HAS(F_CORNELL) {
 #pragma unroll
@@ -374,14 +442,23 @@ __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray
             }
             hr.t = dist; hr.kind = HK_EXAMPLE; hr.idx = 0;
         }
-    } else if HAS(F_MESH) {
-        VR_T1(t_sph, 0);
+        return false;
+    }
+    return HAS(F_MESH);
+}
+
+// intersectScene: closest hit, attributes deferred (fill_hit).
+template <int STACK, bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
+{
+    VR_T0(t_sph);
+    const bool mesh = intersect_spheres<COUNT, FEAT>(p, r, hr, cnt);
+    VR_T1(t_sph, 0);
+    if (mesh) {
         VR_T0(t_mesh);
         traverse_mesh<STACK, COUNT, FEAT>(p, r, hr, L, cnt);
         VR_T1(t_mesh, 1);
-        return hr.t < 1e20f;
     }
-    VR_T1(t_sph, 0);
     return hr.t < 1e20f;
 }
 
@@ -538,138 +615,171 @@ __device__ __forceinline__ uint32_t hash_seeds(uint32_t& s0, uint32_t& s1) {   /
 }
 
 // trace (PathTracer.cu:597-770)
-template <int STACK, bool COUNT, uint32_t FEAT>
-__device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit0, uint32_t& s0, uint32_t& s1,
-                     const Lds& L, Cnt& cnt)
-{
-    vr4 accum = mk4(0.f, 0.f, 0.f, 0.f);
-    vr4 mask = mk4(1.f, 1.f, 1.f, 0.f);
-    float depth = 1.f;
+// State of one path between bounces (trace, PathTracer.cu:597-770).
+struct PathState {
+    vr4 accum, mask;
+    float depth;
+    int bounce;
     Rng rng;
-    rng.seed(hash_seeds(s0, s1));
+};
 
-    for (unsigned bounces = 0; bounces < 4; bounces++) {
-        HitRec hr;
-        bool hit;
-        if (!COUNT && bounces == 0) {
-            // the camera ray is the same for both samples of every frame (no
-            // jitter, PathTracer.cu:842-844): its hit is computed once per pixel
-            hr = hr0;
-            hit = hit0;
+// trace's prologue (:603-622); s0, s1 are updated as the reference's seeds
+__device__ __forceinline__ void path_begin(PathState& ps, uint32_t& s0, uint32_t& s1) {
+    ps.accum = mk4(0.f, 0.f, 0.f, 0.f);
+    ps.mask = mk4(1.f, 1.f, 1.f, 0.f);
+    ps.depth = 1.f;
+    ps.bounce = 0;
+    ps.rng.seed(hash_seeds(s0, s1));
+}
+
+// One bounce of trace's loop body (:627-769) for the closest hit `hr` of
+// `ray` (hr.t == 1e20: miss).  Returns true when the path ends, with its
+// radiance (w = depth) in `out`; otherwise `ray` is the next bounce's ray.
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, const HitRec& hr, PathState& ps,
+                                            vr4& out, Cnt& cnt)
+{
+    const bool hit = hr.t < 1e20f;
+    if (!hit) {
+        if (!HAS(F_CORNELL)) {                                    // :631-648
+            float lx = atan2_p(ray.d.x, ray.d.z);
+            float ly = acos_p(ray.d.y);
+            lx = lx < 0 ? (float)((double)lx + 2.0 * (double)VR_PI) : lx;
+            lx = (float)((double)lx / (2.0 * (double)VR_PI));
+            ly = ly / VR_PI;
+            const int x = f2i(lx * (float)p.hdr_w);
+            const int y = f2i(ly * (float)p.hdr_h);
+            const int val = (int)((uint32_t)x + (uint32_t)y * p.hdr_w);
+            const int addr = (int)clampi(val, 0, (int)(p.hdr_w * p.hdr_h - 1u));
+            if (COUNT) cnt.hdr++;
+            ps.accum = add4(ps.accum, mul4(mul4s(ps.mask, 2.f), p.hdr[addr]));
+            ps.accum.w = ps.depth;
+            out = ps.accum;
+            return true;
+        }
+        out = mk4(0.f, 0.f, 0.f, 0.f);
+        return true;
+    }
+    if (!COUNT && ps.bounce == 3) {
+        // last bounce: only the emission term is observable; the material
+        // branch below would only prepare a ray that is never traced
+        ps.accum = add4(ps.accum, mul4(ps.mask, emission_of(hr)));
+        ps.accum.w = ps.depth;
+        out = ps.accum;
+        return true;
+    }
+    Hit h;
+    VR_T0(t_fill);
+    fill_hit<FEAT>(p, ray, hr, h);
+    VR_T1(t_fill, 2);
+    if (COUNT) {
+        if (hr.kind == HK_MESH) {
+            cnt.attr += 24 + 48;
+            const bool vb = HAS(F_VIEW_BRDF);
+            cnt.tex += (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb);
+            if (HAS(F_TEX_NORM) && dot4(h.tan, h.tan) > VR_EPS) { cnt.attr += 48; cnt.tex++; }
+        } else if (hr.kind == HK_EXAMPLE) {
+            const bool vb = HAS(F_VIEW_BRDF);
+            cnt.tex += (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb) + (HAS(F_TEX_NORM) != 0);
+        }
+    }
+    if (ps.bounce == 0) {
+        const vr4 l = sub4(ray.o, h.hp);
+        ps.depth = __builtin_sqrtf(dot4(l, l)) / 150.f;
+    }
+    ps.accum = add4(ps.accum, mul4(ps.mask, h.em));
+    ray.o = h.hp;
+    const vr4 normal = h.n;
+    VR_T0(t_shade);
+    VR_LANE(4, 5);
+    if (h.type == 0) {                                                   // :671-676
+        ray.d = sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d)));
+        ray.o = add4(ray.o, mul4s(normal, 0.05f));
+    } else if (h.type == 1) {                                            // :678-722
+        const float aoi = dot4(h.n, muls4(-1.f, ray.d));
+        // powf only matters when spec.x != 0: X * 0 == 0 for finite X and
+        // NaN * 0 compares false, so u < fe is false either way.
+        float fe = 0.f;
+        if (h.spec.x != 0.f)
+            fe = ((1.f - p.fresnel_coef) * pow_p(1.f - aoi, p.fresnel_pow) + p.fresnel_coef * 1.f) * h.spec.x;
+        const bool reflect = (ps.rng.uniform() < fe);
+        vr4 newdir;
+        const vr4 w = normal;
+        const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
+        if (reflect) {
+            muleq4(ps.mask, h.spec);
+            newdir = normalize4(sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d))));
         } else {
-            hit = intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, L, cnt);
-        }
-        if (!hit) {
-            if (!HAS(F_CORNELL)) {                                    // :631-648
-                float lx = atan2_p(ray.d.x, ray.d.z);
-                float ly = acos_p(ray.d.y);
-                lx = lx < 0 ? (float)((double)lx + 2.0 * (double)VR_PI) : lx;
-                lx = (float)((double)lx / (2.0 * (double)VR_PI));
-                ly = ly / VR_PI;
-                const int x = f2i(lx * (float)p.hdr_w);
-                const int y = f2i(ly * (float)p.hdr_h);
-                const int val = (int)((uint32_t)x + (uint32_t)y * p.hdr_w);
-                const int addr = (int)clampi(val, 0, (int)(p.hdr_w * p.hdr_h - 1u));
-                if (COUNT) cnt.hdr++;
-                accum = add4(accum, mul4(mul4s(mask, 2.f), p.hdr[addr]));
-                accum.w = depth;
-                return accum;
-            }
-            return mk4(0.f, 0.f, 0.f, 0.f);
-        }
-        if (!COUNT && bounces == 3) {
-            // last bounce: only the emission term is observable; the material
-            // branch below would only prepare a ray that is never traced
-            accum = add4(accum, mul4(mask, emission_of(hr)));
-            break;
-        }
-        Hit h;
-        VR_T0(t_fill);
-        fill_hit<FEAT>(p, ray, hr, h);
-        VR_T1(t_fill, 2);
-        if (COUNT) {
-            if (hr.kind == HK_MESH) {
-                cnt.attr += 24 + 48;
-                const bool vb = HAS(F_VIEW_BRDF);
-                cnt.tex += (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb);
-                if (HAS(F_TEX_NORM) && dot4(h.tan, h.tan) > VR_EPS) { cnt.attr += 48; cnt.tex++; }
-            } else if (hr.kind == HK_EXAMPLE) {
-                const bool vb = HAS(F_VIEW_BRDF);
-                cnt.tex += (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb) + (HAS(F_TEX_NORM) != 0);
-            }
-        }
-        if (bounces == 0) {
-            const vr4 l = sub4(ray.o, h.hp);
-            depth = __builtin_sqrtf(dot4(l, l)) / 150.f;
-        }
-        accum = add4(accum, mul4(mask, h.em));
-        ray.o = h.hp;
-        const vr4 normal = h.n;
-        VR_T0(t_shade);
-        if (h.type == 0) {                                                   // :671-676
-            ray.d = sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d)));
-            ray.o = add4(ray.o, mul4s(normal, 0.05f));
-        } else if (h.type == 1) {                                            // :678-722
-            const float aoi = dot4(h.n, muls4(-1.f, ray.d));
-            // powf only matters when spec.x != 0: X * 0 == 0 for finite X and
-            // NaN * 0 compares false, so u < fe is false either way.
-            float fe = 0.f;
-            if (h.spec.x != 0.f)
-                fe = ((1.f - p.fresnel_coef) * pow_p(1.f - aoi, p.fresnel_pow) + p.fresnel_coef * 1.f) * h.spec.x;
-            const bool reflect = (rng.uniform() < fe);
-            vr4 newdir;
-            const vr4 w = normal;
-            const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
-            if (reflect) {
-                muleq4(mask, h.spec);
-                newdir = normalize4(sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d))));
-            } else {
-                const float rand1 = 2.f * VR_PI * rng.uniform();
-                const float rand2 = rng.uniform();
-                const float rand2s = __builtin_sqrtf(rand2);
-                const vr4 u = normalize4(cross4(axis, w));
-                const vr4 v = cross4(w, u);
-                float sn, cs;
-                sincos_p(rand1, &sn, &cs);
-                newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
-                                         mul4s(w, __builtin_sqrtf(1 - rand2))));
-                muleq4(mask, h.col);
-                muleq4s(mask, dot4(newdir, normal));
-                muleq4s(mask, 2.f);
-            }
-            ray.o = add4(ray.o, mul4s(normal, 0.05f));
-            ray.d = newdir;
-        } else if (h.type == 2) {                                            // :724-764
-            const vr4 w = normal;
-            const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
-            const float rand1 = 2.f * VR_PI * rng.uniform();
-            const float rand2 = rng.uniform();
+            const float rand1 = 2.f * VR_PI * ps.rng.uniform();
+            const float rand2 = ps.rng.uniform();
             const float rand2s = __builtin_sqrtf(rand2);
             const vr4 u = normalize4(cross4(axis, w));
             const vr4 v = cross4(w, u);
             float sn, cs;
             sincos_p(rand1, &sn, &cs);
-            const vr4 newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
-                                               mul4s(w, __builtin_sqrtf(1 - rand2))));
-            if HAS(F_BRDF) {
-                const float dw = 24 * pow_p(newdir.x * newdir.x + newdir.y * newdir.y + newdir.z * newdir.z, -1.5f);
-                if (COUNT) cnt.brdf++;
-                const vr4 b = lookup_brdf(p.brdf, newdir, ray.d, h.n, h.tan);
-                const vr4 bm = mk4(__builtin_fmaxf(b.x, 0.f), __builtin_fmaxf(b.y, 0.f), __builtin_fmaxf(b.z, 0.f),
-                                   __builtin_fmaxf(b.w, 0.f));
-                muleq4(mask, muls4(dw, bm));
-            } else {
-                muleq4(mask, h.col);
-                muleq4s(mask, dot4(newdir, normal));
-                muleq4s(mask, 2.f);
-            }
-            ray.o = add4(ray.o, mul4s(normal, 0.05f));
-            ray.d = newdir;
+            newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
+                                     mul4s(w, __builtin_sqrtf(1 - rand2))));
+            muleq4(ps.mask, h.col);
+            muleq4s(ps.mask, dot4(newdir, normal));
+            muleq4s(ps.mask, 2.f);
         }
-        VR_T1(t_shade, 3);
+        ray.o = add4(ray.o, mul4s(normal, 0.05f));
+        ray.d = newdir;
+    } else if (h.type == 2) {                                            // :724-764
+        const vr4 w = normal;
+        const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
+        const float rand1 = 2.f * VR_PI * ps.rng.uniform();
+        const float rand2 = ps.rng.uniform();
+        const float rand2s = __builtin_sqrtf(rand2);
+        const vr4 u = normalize4(cross4(axis, w));
+        const vr4 v = cross4(w, u);
+        float sn, cs;
+        sincos_p(rand1, &sn, &cs);
+        const vr4 newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
+                                           mul4s(w, __builtin_sqrtf(1 - rand2))));
+        if HAS(F_BRDF) {
+            const float dw = 24 * pow_p(newdir.x * newdir.x + newdir.y * newdir.y + newdir.z * newdir.z, -1.5f);
+            if (COUNT) cnt.brdf++;
+            const vr4 b = lookup_brdf(p.brdf, newdir, ray.d, h.n, h.tan);
+            const vr4 bm = mk4(__builtin_fmaxf(b.x, 0.f), __builtin_fmaxf(b.y, 0.f), __builtin_fmaxf(b.z, 0.f),
+                               __builtin_fmaxf(b.w, 0.f));
+            muleq4(ps.mask, muls4(dw, bm));
+        } else {
+            muleq4(ps.mask, h.col);
+            muleq4s(ps.mask, dot4(newdir, normal));
+            muleq4s(ps.mask, 2.f);
+        }
+        ray.o = add4(ray.o, mul4s(normal, 0.05f));
+        ray.d = newdir;
     }
-    accum.w = depth;
-    return accum;
+    VR_T1(t_shade, 3);
+    if (++ps.bounce == 4) {
+        ps.accum.w = ps.depth;
+        out = ps.accum;
+        return true;
+    }
+    return false;
+}
+
+template <int STACK, bool COUNT, uint32_t FEAT>
+__device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit0, uint32_t& s0, uint32_t& s1,
+                     const Lds& L, Cnt& cnt)
+{
+    PathState ps;
+    path_begin(ps, s0, s1);
+    for (;;) {
+        HitRec hr;
+        if (!COUNT && ps.bounce == 0) {
+            // the camera ray is the same for both samples of every frame (no
+            // jitter, PathTracer.cu:842-844): its hit is computed once per pixel
+            hr = hr0;
+            (void)hit0;
+        } else {
+            (void)intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, L, cnt);
+        }
+        vr4 out;
+        if (bounce_step<COUNT, FEAT>(p, ray, hr, ps, out, cnt)) return out;
+    }
 }
 
 // colour of the accumulated radiance after `frame` frames (PathTracer.cu:850-866)
@@ -714,6 +824,40 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     p.accum[ind] = io;
 }
 
+// Binds this thread's stack column and fills the block's node cache with
+// the first nodes of the area-ordered node array.
+template <uint32_t FEAT>
+__device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, vr4* lds_nodes, int2* lds_idx,
+                                         int cn, int tid)
+{
+    Lds L;
+    L.stk = lds_stack + tid;
+    L.nodes = lds_nodes;
+    L.idx = lds_idx;
+    L.n_cached = 0;
+#ifndef VR_NO_NODE_CACHE
+    if (HAS(F_MESH)) {
+        L.n_cached = (int)(p.n_nodes < (uint32_t)cn ? p.n_nodes : (uint32_t)cn);
+        for (int i = tid; i < 3 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh[(i / 3) * 4 + i % 3];
+        for (int i = tid; i < L.n_cached; i += kBlockThreads)
+            lds_idx[i] = *reinterpret_cast<const int2*>(p.bvh + 4 * i + 3);
+        __syncthreads();
+    }
+#endif
+    return L;
+}
+
+// Camera ray through pixel (x, y) (PathTracer.cu:842-844: no jitter).
+__device__ __forceinline__ Ray camera_ray(const RenderParams& p, uint32_t x, uint32_t y)
+{
+    const float sx = (float)((0.25 + (double)x) / (double)p.W - 0.5);
+    const float sy = (float)((0.25 + (double)y) / (double)p.H - 0.5);
+    Ray cam;
+    cam.o = p.cam_o;
+    cam.d = normalize4(add4(add4(p.cam_d, mul4s(p.cx, sx)), mul4s(p.cy, sy)));
+    return cam;
+}
+
 // render (PathTracer.cu:791-868), K frames per launch.
 #ifndef VR_MIN_WAVES_PER_SIMD
 #define VR_MIN_WAVES_PER_SIMD 4
@@ -726,20 +870,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
     const int tid = threadIdx.x;
-    Lds L;
-    L.stk = lds_stack + tid;
-    L.nodes = lds_nodes;
-    L.idx = lds_idx;
-    L.n_cached = 0;
-#ifndef VR_NO_NODE_CACHE
-    if (HAS(F_MESH)) {
-        L.n_cached = (int)(p.n_nodes < (uint32_t)CN ? p.n_nodes : (uint32_t)CN);
-        for (int i = tid; i < 3 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh[(i / 3) * 4 + i % 3];
-        for (int i = tid; i < L.n_cached; i += kBlockThreads)
-            lds_idx[i] = *reinterpret_cast<const int2*>(p.bvh + 4 * i + 3);
-        __syncthreads();
-    }
-#endif
+    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
     // block -> (tile, path group): the 2*n_frames paths of a pixel are split
     // into p.split contiguous groups run by different blocks (strong-scaling
     // and tail balance); group g of tile t is block t*split + g
@@ -757,11 +888,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     VR_T0(t_kernel);
 
     const uint32_t ind = x + y * p.W;
-    const float sx = (float)((0.25 + (double)x) / (double)p.W - 0.5);   // :842
-    const float sy = (float)((0.25 + (double)y) / (double)p.H - 0.5);
-    Ray cam;
-    cam.o = p.cam_o;
-    cam.d = normalize4(add4(add4(p.cam_d, mul4s(p.cx, sx)), mul4s(p.cy, sy)));
+    const Ray cam = camera_ray(p, x, y);
     HitRec hr0;
     bool hit0 = false;
     if (!COUNT) hit0 = intersect_scene<STACK, COUNT, FEAT>(p, cam, hr0, L, cnt);
@@ -772,7 +899,8 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     const uint32_t chunk = (n_paths + T - 1u) / T;
     const uint32_t q0 = g * chunk;
     const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
-    vr4 io = (T == 1u && p.first_frame != 1u) ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
+    const bool direct = !p.use_scratch;                  // accumulate here (counting launches)
+    vr4 io = (direct && p.first_frame != 1u) ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
     uint32_t s1 = 0, s2 = 0;
     float last_w = 0.f;
 #pragma unroll 1
@@ -784,23 +912,24 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
             if (q & 1u) (void)hash_seeds(s1, s2);
         }
         const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, L, cnt);
-        if (T == 1u)
+        if (direct)
             io = add4(io, mul4s(result, 1.f / 2.f));
         else
             p.paths[(size_t)q * p.path_stride + (size_t)tile * kBlockThreads + tid] = result;
         last_w = result.w;
     }
-    if (T != 1u) return;   // finish_kernel accumulates the groups' results in path order
-    VR_T0(t_tone);
-    // only the launch's last frame is observable in the colour and depth
-    // surfaces (each frame of the reference overwrites them, :846-866)
-    const unsigned char db = f2u8((1.f - last_w) * 255);
-    u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
-    p.depth[ind] = dv;
-    p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
-    p.accum[ind] = io;
-    VR_T1(t_tone, 4);
-#ifdef VR_TIMING
+    if (direct) {   // else finish_kernel accumulates the paths' results in path order
+        VR_T0(t_tone);
+        // only the launch's last frame is observable in the colour and depth
+        // surfaces (each frame of the reference overwrites them, :846-866)
+        const unsigned char db = f2u8((1.f - last_w) * 255);
+        u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
+        p.depth[ind] = dv;
+        p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
+        p.accum[ind] = io;
+        VR_T1(t_tone, 4);
+    }
+#if defined(VR_TIMING) || defined(VR_LANESTATS)
     VR_T1(t_kernel, 5);
     if (p.counters) {
 #pragma unroll
@@ -823,6 +952,137 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
             if (lane == 0 && x) atomicAdd(p.counters + k, x);
         }
     }
+}
+
+// Path-pool variant of render (the default): each wave owns the paths
+// [q0, q1) of its 8x8 sub-tile's 64 pixels as a pool of 64*(q1-q0) items
+// (item i: pixel i % 64, path q0 + i / 64).  A lane runs one path at a time;
+// when its path ends it stores the path's radiance to p.paths and takes the
+// next item of the pool, so lanes whose rays finish early do not idle while
+// the wave's other lanes traverse.  Traversal is paused between outer
+// iterations (trav_iter) once VR_SHADE_BATCH lanes wait for shading.  Every
+// path runs exactly the operations of trace(); only the interleaving of
+// different paths on the SIMD changes, so results are bit-identical.
+// finish_kernel then sums each pixel's paths in path order.
+// Traversal pauses for shading once VR_SHADE_BATCH lanes wait for it and
+// they are at least 1/VR_SHADE_RATIO of the lanes still traversing
+// (measured on C2/C3: 16 and 1; the choice moves results by < 1 %).
+#ifndef VR_SHADE_BATCH
+#define VR_SHADE_BATCH 16
+#endif
+#ifndef VR_SHADE_RATIO
+#define VR_SHADE_RATIO 1
+#endif
+enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3 };
+
+template <int STACK, uint32_t FEAT>
+__global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_wave_kernel(const RenderParams p)
+{
+    constexpr int CN = cache_nodes(STACK);
+    __shared__ int lds_stack[STACK * kBlockThreads];
+    __shared__ vr4 lds_nodes[3 * CN];
+    __shared__ int2 lds_idx[CN];
+    const int tid = threadIdx.x;
+    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
+    const uint32_t T = p.split;
+    const uint32_t tile = blockIdx.x / T;
+    const uint32_t g = blockIdx.x - tile * T;
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t x0 = tile_x * 16u + (uint32_t)((wave & 1) * 8);
+    const uint32_t y0 = tile_y * 16u + (uint32_t)((wave >> 1) * 8);
+    const uint32_t n_paths = 2u * p.n_frames;
+    const uint32_t chunk = (n_paths + T - 1u) / T;
+    const uint32_t q0 = g * chunk < n_paths ? g * chunk : n_paths;
+    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
+    const uint32_t pool = 64u * (q1 - q0);
+    vr4* const out_base = p.paths + (size_t)tile * kBlockThreads + (size_t)wave * 64u;
+    Cnt cnt;
+
+    uint32_t item = (uint32_t)lane;
+    uint32_t next = 64u;                                   // wave-uniform: first unassigned item
+    int state = LS_DONE;
+    Ray ray;
+    PathState ps;
+    HitRec hr;
+    Trav tr;
+    auto start = [&]() {                                   // render's per-sample prologue (:817-844)
+        const uint32_t px = item & 63u, q = q0 + (item >> 6), f = q >> 1;
+        const uint32_t x = x0 + (px & 7u), y = y0 + (px >> 3);
+        uint32_t s1 = x * (p.first_frame + f);
+        uint32_t s2 = y * p.times[f];
+        if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
+        path_begin(ps, s1, s2);
+        ray = camera_ray(p, x, y);
+        state = LS_SETUP;
+    };
+    if (item < pool) start();
+
+    for (;;) {
+        if (state == LS_SETUP) {
+            if (intersect_spheres<false, FEAT>(p, ray, hr, cnt)) {
+                trav_init<FEAT>(p, ray, hr.t, tr, L);
+                state = LS_TRAV;
+            } else {
+                state = LS_SHADE;
+            }
+        }
+        if (HAS(F_MESH)) {
+            for (;;) {
+                const int n_trav = __popcll(__ballot(state == LS_TRAV));
+                if (n_trav == 0) break;
+                const int n_shade = __popcll(__ballot(state == LS_SHADE));
+                if (n_shade >= VR_SHADE_BATCH && n_shade * VR_SHADE_RATIO >= n_trav) break;
+                if (state == LS_TRAV) {
+#ifdef VR_IFIF
+                    trav_step<false, FEAT>(p, ray, tr, L, cnt);
+                    if (tr.nodeAddr == kSentinel && tr.k >= tr.kend) {
+#else
+                    trav_iter<STACK, false, FEAT>(p, ray, tr, L, cnt);
+                    if (tr.nodeAddr == kSentinel) {
+#endif
+                        trav_finish(tr, hr);
+                        state = LS_SHADE;
+                    }
+                }
+            }
+        }
+        bool ended = false;
+        if (state == LS_SHADE) {
+            VR_LANE(4, 5);
+            vr4 out;
+            if (bounce_step<false, FEAT>(p, ray, hr, ps, out, cnt)) {
+                out_base[(size_t)(q0 + (item >> 6)) * p.path_stride + (item & 63u)] = out;
+                ended = true;
+            } else {
+                state = LS_SETUP;
+            }
+        }
+        const unsigned long long em = __ballot(ended);
+        if (em != 0ull) {
+            if (ended) {
+                item = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                if (item < pool) start();
+                else state = LS_DONE;
+            }
+            next += (uint32_t)__popcll(em);
+        }
+        if (__ballot(state != LS_DONE) == 0ull) break;
+    }
+#ifdef VR_LANESTATS
+    if (p.counters) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            unsigned long long v = cnt.tm[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+            if (lane == 0) atomicAdd(p.counters + 8 + k, v);
+        }
+    }
+#endif
 }
 
 // ---- small helper kernels ------------------------------------------------
@@ -889,10 +1149,19 @@ static void launch_spec(const RenderParams& p, uint32_t blocks, int stack_depth,
 #ifndef VR_MIN_SPEC_STACK
 #define VR_MIN_SPEC_STACK 16
 #endif
-    if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
+    // mesh scenes: the path-pool kernel (traversal divergence); sphere-only
+    // scenes: one pixel per thread, primary hit shared by its paths
+#ifdef VR_CLASSIC_KERNEL
+    const bool wave = false;
+#else
+    const bool wave = (FEAT & F_MESH) != 0 && (p.flags & F_MESH) != 0;
+#endif
+    if (!wave)
         hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+    else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
+        hipLaunchKernelGGL((render_wave_kernel<16, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
     else
-        hipLaunchKernelGGL((render_kernel<32, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+        hipLaunchKernelGGL((render_wave_kernel<32, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
 }
 
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream)
@@ -907,7 +1176,7 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool
             if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
             else hipLaunchKernelGGL((render_kernel<64, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
         } else {
-            hipLaunchKernelGGL((render_kernel<64, false, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+            hipLaunchKernelGGL((render_wave_kernel<64, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
         }
     } else if (covers(kFeatCornellMesh)) {
         launch_spec<kFeatCornellMesh>(p, blocks, stack_depth, s);
@@ -927,7 +1196,7 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool
 
 int launch_finish(const RenderParams& p, uint32_t n_tiles, void* stream)
 {
-    if (n_tiles == 0 || p.split <= 1u) return 0;
+    if (n_tiles == 0 || !p.use_scratch) return 0;
     hipLaunchKernelGGL(finish_kernel, dim3(n_tiles), dim3(kBlockThreads), 0, (hipStream_t)stream, p);
     return (int)hipGetLastError();
 }

@@ -39,9 +39,10 @@ struct RenderParams {
     uint32_t tiles_x;                // wr / 16
     uint32_t rank, nranks;           // 16x16 tiles dealt round-robin: rank owns tiles rank + j*nranks
     uint32_t first_frame, n_frames;
-    uint32_t split;                  // path groups per pixel (1: a thread runs all 2*n_frames paths)
-    uint32_t path_stride;            // split > 1: owned tiles * 256 (scratch row length)
-    vr4* paths;                      // split > 1: per-path results [2*n_frames][path_stride]
+    uint32_t split;                  // path groups per pixel (blocks per tile)
+    uint32_t use_scratch;            // 1: paths store radiance to `paths`, finish_kernel accumulates
+    uint32_t path_stride;            // owned tiles * 256 (scratch row length)
+    vr4* paths;                      // per-path results [2*n_frames][path_stride]
     const vr4* bvh;
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
     const vr3* verts;                // 3 vertices per triangle, compact leaf order
@@ -63,7 +64,7 @@ struct RenderParams {
 
 // host-side launchers implemented in vr_kernel.hip
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream);
-// split launches only: sums the per-path results of launch_render in path order
+// use_scratch launches: sums the per-path results of launch_render in path order
 int launch_finish(const RenderParams& p, uint32_t n_tiles, void* stream);
 int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);
 int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,

@@ -524,7 +524,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
         p.counters = c->counters;
     }
-#ifdef VR_TIMING
+#if defined(VR_TIMING) || defined(VR_LANESTATS)
     if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
     p.counters = c->counters;   // diagnostic build: phase timers in slots 8..13
 #endif
@@ -532,7 +532,8 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     const uint32_t k_max = std::min<uint32_t>(n_frames, (uint32_t)vr::kMaxFramesPerLaunch);
     const uint32_t split_max = count ? 1u : choose_split(c, n_tiles, k_max);
     p.path_stride = n_tiles * (uint32_t)vr::kBlockThreads;
-    if (split_max > 1u) {
+    p.use_scratch = count ? 0u : 1u;   // the counting variant accumulates in place
+    if (p.use_scratch) {
         const size_t need = (size_t)2 * k_max * p.path_stride;
         if (need > c->paths_cap) {
             dfree(c->paths);
