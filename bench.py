@@ -90,10 +90,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # VRHIP_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
+    # on one GPU (host-staged gather); the measured configuration is "nccl"
+    # (RCCL over xGMI), one rank per GPU
+    backend = os.environ.get("VRHIP_DIST_BACKEND", "nccl")
+    gpu = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from vrenderer_pathtracer_amd import VRendererHIP, build_native, scenes
     from vrenderer_pathtracer_amd.tiles import TileGather, WHAT_RGBA8
@@ -102,9 +111,12 @@ def main():
     W, H = scene["width"], scene["height"]
     F = args.frames_per_step
 
-    r = VRendererHIP(local_rank)
+    r = VRendererHIP(gpu)
     scenes.load_into(r, scene)
-    stream = torch.cuda.current_stream(dev)
+    # one non-default stream shared by the renderer and torch (the collective
+    # is ordered after the pack kernel by torch's stream semantics)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     r.set_tiling(rank, world)
     owned = r.owned_pixels()
@@ -138,14 +150,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kms, launches = r.kernel_stats()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
     # aggregate counts over ranks
     keys = sorted(counts)
-    cvec = torch.tensor([counts[k] for k in keys] + [owned], dtype=torch.float64, device=dev)
+    cvec = torch.tensor([counts[k] for k in keys] + [owned], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(cvec)
     tot = {k: float(v) for k, v in zip(keys + ["owned_pixels"], cvec.tolist())}

@@ -273,6 +273,10 @@ class VRendererHIP:
     def set_stream(self, stream_handle) -> None:
         check(self._lib.vrhip_set_stream(self._need_ctx(), ctypes.c_void_p(stream_handle)), "vrhip_set_stream")
 
+    def get_stream(self) -> int:
+        """hipStream_t the context enqueues on (as an integer handle)."""
+        return int(self._lib.vrhip_get_stream(self._need_ctx()) or 0)
+
     def sync(self) -> None:
         check(self._lib.vrhip_sync(self._need_ctx()), "vrhip_sync")
 

@@ -65,25 +65,41 @@ class TileGather:
 
     renderer: VRendererHIP with set_tiling(rank, world) applied; torch tensors
     hold the send/receive buffers on the renderer's device so the collective
-    runs over RCCL; rank 0's renderer receives the full image.
+    runs over RCCL (backend "nccl"); rank 0's renderer receives the full
+    image.  With the gloo backend (CPU rehearsal of the multi-rank path on one
+    GPU) the buffers are staged through host memory.
     """
 
     def __init__(self, renderer, rank: int, world: int, device, what: int = WHAT_RGBA8):
         import torch
+        import torch.distributed as dist
         self.r, self.rank, self.world, self.what = renderer, rank, world, what
+        self.device = device
         H, W = renderer.height, renderer.width
         self.stride = max_owned_pixels(W, H, world) * _ELEM_BYTES[what]
         self.send = torch.empty(self.stride, dtype=torch.uint8, device=device)
         self.recv = None
+        self.host = world > 1 and dist.get_backend() == "gloo"
         if rank == 0 and world > 1:
             self.recv = torch.empty(world * self.stride, dtype=torch.uint8, device=device)
-            self.views = list(self.recv.view(world, self.stride).unbind(0))
+            views = self.recv.cpu() if self.host else self.recv
+            self.recv_stage = views
+            self.views = list(views.view(world, self.stride).unbind(0))
 
     def step(self) -> None:
+        import torch
         import torch.distributed as dist
         if self.world == 1:
             return
+        own_stream = self.r.get_stream() != torch.cuda.current_stream(self.device).cuda_stream
         self.r.pack_tiles(self.what, self.send.data_ptr())
-        dist.gather(self.send, self.views if self.rank == 0 else None, dst=0)
+        if own_stream or self.host:
+            self.r.sync()                     # the collective reads `send` on torch's stream
+        send = self.send.cpu() if self.host else self.send
+        dist.gather(send, self.views if self.rank == 0 else None, dst=0)
         if self.rank == 0:
+            if self.host:
+                self.recv.copy_(self.recv_stage)
+            if own_stream or self.host:
+                torch.cuda.current_stream(self.device).synchronize()
             self.r.unpack_tiles(self.what, self.recv.data_ptr(), self.world, self.stride)
