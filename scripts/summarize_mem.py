@@ -5,6 +5,7 @@ the bench's render kernel into profiles/<name>_mem.md.
   python scripts/summarize_mem.py gpurun_out/prof_<tag> <name>
 """
 import csv
+import re
 import glob
 import os
 import sys
@@ -19,7 +20,7 @@ def main():
     for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
-            if "render_kernel" in k and "true" not in k:
+            if re.search(r"render_(wave_|block_)?kernel", k) and "true" not in k:
                 vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
     m = {k: sum(v) / len(v) for k, v in vals.items()}
     cus = 256

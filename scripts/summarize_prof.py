@@ -14,6 +14,7 @@ so the read side is doubled (an upper bound for this gather pattern, whose
 calibration is unmeasured -- noted in the summary).
 """
 import csv
+import re
 import glob
 import json
 import os
@@ -28,7 +29,7 @@ def pmc_means(d):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if "render_kernel" in row["Kernel_Name"] and "true" not in row["Kernel_Name"]:
+            if re.search(r"render_(wave_|block_)?kernel", row["Kernel_Name"]) and "true" not in row["Kernel_Name"]:
                 vals[(row["Kernel_Name"], row["Counter_Name"])].append(float(row["Counter_Value"]))
     return {f"{k[0]}|{k[1]}": sum(v) / len(v) for k, v in vals.items()}
 
@@ -45,7 +46,7 @@ def main():
     for sub in ("prof_fetch", "prof_write", "prof_sq"):
         pmc.update(pmc_means(os.path.join(src, sub)))
     json.dump(pmc, open(os.path.join(prof, f"{name}_pmc.json"), "w"), indent=1, sort_keys=True)
-    kern = [r for r in rows if "render_kernel" in r["Name"] and "true" not in r["Name"]]
+    kern = [r for r in rows if re.search(r"render_(wave_|block_)?kernel", r["Name"]) and "true" not in r["Name"]]
     fetch = [v for k, v in pmc.items() if k.endswith("|FETCH_SIZE")]
     write = [v for k, v in pmc.items() if k.endswith("|WRITE_SIZE")]
     traffic = None

@@ -5,7 +5,7 @@
 // in vRendererCuda::initMesh (src/vRendererCuda.cpp:204-279).  The kernel's
 // closest hit does not depend on the tree shape (no t-culling in the
 // reference traversal, PathTracer.cu:316,322), so any valid tree renders the
-// same image; this file builds a binned-SAH tree (object splits, 32 bins per
+// same image; this file builds a binned-SAH tree (object splits, 128 bins per
 // axis, SAH costs kNodeCost = kTriangleCost = 1 as in the reference) and
 // writes it in exactly the reference's flattened layout:
 //   node (4 float4): (c0.minx,c0.maxx,c0.miny,c0.maxy) (c1.minx,c1.maxx,c1.miny,c1.maxy)
@@ -59,7 +59,13 @@ struct Builder {
     std::vector<uint32_t> refs;        // triangle references (leaf ranges index this)
     std::vector<BuildNode> nodes;
 
-    static constexpr int kBins = 32;
+#ifndef VR_BVH_BINS
+#define VR_BVH_BINS 128
+#endif
+#ifndef VR_BVH_NODE_COST
+#define VR_BVH_NODE_COST 1.0
+#endif
+    static constexpr int kBins = VR_BVH_BINS;
 
     int make_leaf(uint32_t first, uint32_t count, const Box& b) {
         BuildNode n; n.box = b; n.first = first; n.count = count; n.leaf = true;
@@ -110,7 +116,7 @@ struct Builder {
         }
         const double parent_area = b.area();
         // SAH: C_node + (A_L N_L + A_R N_R) / A_P * C_tri  vs  N * C_tri
-        const double split_cost = 1.0 + (parent_area > 0.0 ? best_cost / parent_area : (double)count);
+        const double split_cost = VR_BVH_NODE_COST + (parent_area > 0.0 ? best_cost / parent_area : (double)count);
         const bool want_leaf = count <= max_leaf && (best_axis < 0 || split_cost >= (double)count);
         if (!force_split && want_leaf) return make_leaf(first, count, b);
 
@@ -159,7 +165,12 @@ int build_flat(const float* positions, const float* normals, const float* tangen
         if (tris[i] >= n_verts) return -1;
     Builder B;
     B.pos = positions; B.tris = tris;
+#ifdef VR_BVH_MAX_LEAF
+    (void)max_leaf_tris;
+    B.max_leaf = VR_BVH_MAX_LEAF;
+#else
     B.max_leaf = max_leaf_tris ? max_leaf_tris : 4;
+#endif
     B.max_depth = kMaxBuildDepth;
     B.tri_box.resize(n_tris);
     B.centroid.resize(3 * (size_t)n_tris);

@@ -177,8 +177,10 @@ constexpr int kLeafCountBits = 7;
 #define VR_LDS_BUDGET (40960 - 256)
 #endif
 constexpr int kLdsBudget = VR_LDS_BUDGET;
-constexpr int cache_nodes(int stack) { return (kLdsBudget - stack * kBlockThreads * 4) / 56 > 0 ?
-                                              (kLdsBudget - stack * kBlockThreads * 4) / 56 : 1; }
+constexpr int cache_nodes(int stack, int extra = 0) {
+    return (kLdsBudget - stack * kBlockThreads * 4 - extra) / 56 > 0 ?
+           (kLdsBudget - stack * kBlockThreads * 4 - extra) / 56 : 1;
+}
 // Raw buffer loads for the node and triangle arrays: a 32-bit lane offset
 // against an SGPR descriptor (bounds-checked, no 64-bit address math), and an
 // explicit width per fetch (16 B node rows, 8 B child indices, 12 B vertices).
@@ -203,8 +205,8 @@ __device__ __forceinline__ int2 buf_load2i(__amdgpu_buffer_rsrc_t b, int off) {
 
 struct Lds {
     int* stk;                 // this thread's column of the stack
-    const vr4* nodes;         // 3 rows per cached node
-    const int2* idx;          // child indices per cached node
+    const vr4* nodes;         // fp32 nodes: 3 rows per cached node; fp16 nodes: 2 rows per node
+    const int2* idx;          // fp32 nodes: child indices per cached node
     int n_cached;             // nodes [0, n_cached) are read from LDS
 };
 
@@ -217,6 +219,7 @@ struct Trav {
     float ivx, ivy, ivz, odx, ody, odz;
     float t, tcull, bu, bv;
     int best, sp, nodeAddr;
+    int top;                  // register copy of the stack top, stk[sp]
     int k, kend;              // leaf in progress (trav_step only)
 };
 
@@ -225,6 +228,7 @@ __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, f
 {
     tr.sp = 0;
     L.stk[0] = kSentinel;
+    tr.top = kSentinel;
     tr.nodeAddr = 0;
     tr.ivx = 1.f / (__builtin_fabsf(r.d.x) > VR_EPS ? r.d.x : VR_EPS);
     tr.ivy = 1.f / (__builtin_fabsf(r.d.y) > VR_EPS ? r.d.y : VR_EPS);
@@ -244,6 +248,21 @@ __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, f
 // One outer iteration: the inner node loop until this lane holds a leaf and
 // the wave agrees (ballot), then the leaf loop.  Precondition: tr.nodeAddr is
 // an inner node (not kSentinel).
+// Pop (:339-342 and the leaf-loop pops): the top is already in a register;
+// the entry below it is read for the next pop, off the critical path.  sp
+// reaches -1 only by popping the sentinel, after which nothing is popped.
+__device__ __forceinline__ int trav_pop(Trav& tr, const int* stk)
+{
+#ifdef VR_TOP_IN_REG
+    const int v = tr.top;
+    --tr.sp;
+    tr.top = stk[(tr.sp > 0 ? tr.sp : 0) * kBlockThreads];
+    return v;
+#else
+    return stk[(tr.sp--) * kBlockThreads];
+#endif
+}
+
 // One inner-node visit (:295-343): fetch (LDS copy or L2/HBM), two slab
 // tests, near child next, far child pushed when both are entered, pop when
 // neither is.  Leaves in tr.nodeAddr are left to the caller.
@@ -251,27 +270,55 @@ template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
     int* stk = L.stk;
-    const __amdgpu_buffer_rsrc_t nbuf = buf_rsrc(p.bvh, p.n_nodes * 64u);
     const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
     if (COUNT) cnt.nodes++;
     VR_LANE(0, 1);
     vr4 n0, n1, nz;
-    int2 ni;
+    int idx0, idx1;
     const int node = tr.nodeAddr >> 2;
-    // wave-uniform choice: a diverged wave would pay both round trips
-    if (__ballot(node >= L.n_cached) == 0ull) {
-        n0 = L.nodes[3 * node + 0];
-        n1 = L.nodes[3 * node + 1];
-        nz = L.nodes[3 * node + 2];
-        ni = L.idx[node];
+    // wave-uniform choice between the LDS copy and L2/HBM: a diverged wave
+    // would pay both round trips
+    const bool in_lds = __ballot(node >= L.n_cached) == 0ull;
+    if (!strict) {
+        // conservative fp16 boxes (lows rounded down, highs up): two 16-B
+        // fetches per node instead of four; a box can only grow, so no hit
+        // the exact box admits is lost
+        vr4 a, b;
+        if (in_lds) {
+            a = L.nodes[2 * node];
+            b = L.nodes[2 * node + 1];
+        } else {
+            const __amdgpu_buffer_rsrc_t hbuf = buf_rsrc(p.bvh16, p.n_nodes * 32u);
+            const int off = node * 32;
+            a = buf_load4(hbuf, off);
+            b = buf_load4(hbuf, off + 16);
+        }
+        auto lo = [](float w) { return __half2float(__ushort_as_half((unsigned short)(__float_as_uint(w) & 0xffffu))); };
+        auto hi = [](float w) { return __half2float(__ushort_as_half((unsigned short)(__float_as_uint(w) >> 16))); };
+        n0 = mk4(lo(a.x), hi(a.x), lo(a.y), hi(a.y));          // c0 x, y
+        nz = mk4(lo(a.z), hi(a.z), lo(b.y), hi(b.y));          // c0 z, c1 z
+        n1 = mk4(lo(a.w), hi(a.w), lo(b.x), hi(b.x));          // c1 x, y
+        idx0 = __float_as_int(b.z);
+        idx1 = __float_as_int(b.w);
     } else {
-        const int off = tr.nodeAddr * 16;                     // byte offset of the node
-        n0 = buf_load4(nbuf, off);
-        n1 = buf_load4(nbuf, off + 16);
-        nz = buf_load4(nbuf, off + 32);
-        ni = buf_load2i(nbuf, off + 48);                      // 8 of the row's 16 bytes are used
+        int2 ni;
+        if (in_lds) {
+            const int row = __mul24(3, node);                 // v_mul_u32_u24 (full rate)
+            n0 = L.nodes[row + 0];
+            n1 = L.nodes[row + 1];
+            nz = L.nodes[row + 2];
+            ni = L.idx[node];
+        } else {
+            const __amdgpu_buffer_rsrc_t nbuf = buf_rsrc(p.bvh, p.n_nodes * 64u);
+            const int off = tr.nodeAddr * 16;                 // byte offset of the node
+            n0 = buf_load4(nbuf, off);
+            n1 = buf_load4(nbuf, off + 16);
+            nz = buf_load4(nbuf, off + 32);
+            ni = buf_load2i(nbuf, off + 48);                  // 8 of the row's 16 bytes are used
+        }
+        idx0 = ni.x;
+        idx1 = ni.y;
     }
-    const int idx0 = ni.x, idx1 = ni.y;
     // slab distances n*inv - o*inv (:307-322); the culled mode lets
     // them contract to one v_fma each (more accurate)
     auto slab = [&](float n, float iv, float od) {
@@ -302,12 +349,23 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     // are hit, pop when neither is (same order as :324-343)
     const bool both = tc0 && tc1;
     const bool none = !tc0 && !tc1;
-    const int top = stk[tr.sp * kBlockThreads];
     const int nearc = (both && swp) ? idx1 : (tc0 ? idx0 : idx1);
     const int farc = swp ? idx0 : idx1;
+#ifdef VR_TOP_IN_REG
+    // branch-free, stack top in a register: the entry below the new top is
+    // read every visit but only consumed by a later pop
+    const int popped = tr.top;
+    if (both) stk[(tr.sp + 1) * kBlockThreads] = farc;
+    tr.sp += both ? 1 : (none ? -1 : 0);
+    tr.nodeAddr = none ? popped : nearc;
+    const int below = stk[(tr.sp > 0 ? tr.sp : 0) * kBlockThreads];
+    tr.top = both ? farc : (none ? below : tr.top);
+#else
+    const int top = stk[tr.sp * kBlockThreads];
     if (both) stk[(tr.sp + 1) * kBlockThreads] = farc;
     tr.sp += both ? 1 : (none ? -1 : 0);
     tr.nodeAddr = none ? top : nearc;
+#endif
 }
 
 // intersectTriangle (RayIntersection.cuh:54-111) for compact triangle k and
@@ -357,8 +415,7 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         node_step<COUNT, FEAT>(p, r, tr, L, cnt);
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
             leafAddr = tr.nodeAddr;
-            tr.nodeAddr = stk[tr.sp * kBlockThreads];
-            --tr.sp;
+            tr.nodeAddr = trav_pop(tr, stk);
         }
         if (__ballot(leafAddr >= 0) == 0ull) break;          // every lane holds a leaf
     }
@@ -367,10 +424,7 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
         for (int k = lv >> kLeafCountBits; k < kend; ++k) tri_test<COUNT, FEAT>(p, r, tr, k, cnt);
         leafAddr = tr.nodeAddr;
-        if (tr.nodeAddr < 0) {
-            tr.nodeAddr = stk[tr.sp * kBlockThreads];
-            --tr.sp;
-        }
+        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop(tr, stk);
     }
 }
 
@@ -391,8 +445,7 @@ __device__ __forceinline__ void trav_step(const RenderParams& p, const Ray& r, T
         const int lv = ~tr.nodeAddr;
         tr.k = lv >> kLeafCountBits;
         tr.kend = tr.k + (lv & ((1 << kLeafCountBits) - 1));
-        tr.nodeAddr = L.stk[tr.sp * kBlockThreads];
-        --tr.sp;
+        tr.nodeAddr = trav_pop(tr, L.stk);
     }
 }
 
@@ -837,10 +890,16 @@ __device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, 
     L.n_cached = 0;
 #ifndef VR_NO_NODE_CACHE
     if (HAS(F_MESH)) {
-        L.n_cached = (int)(p.n_nodes < (uint32_t)cn ? p.n_nodes : (uint32_t)cn);
-        for (int i = tid; i < 3 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh[(i / 3) * 4 + i % 3];
-        for (int i = tid; i < L.n_cached; i += kBlockThreads)
-            lds_idx[i] = *reinterpret_cast<const int2*>(p.bvh + 4 * i + 3);
+        if (!HAS(F_STRICT)) {                          // fp16 nodes, 32 B: 1.5x as many fit
+            const uint32_t cap = (uint32_t)(3 * cn / 2);
+            L.n_cached = (int)(p.n_nodes < cap ? p.n_nodes : cap);
+            for (int i = tid; i < 2 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh16[i];
+        } else {
+            L.n_cached = (int)(p.n_nodes < (uint32_t)cn ? p.n_nodes : (uint32_t)cn);
+            for (int i = tid; i < 3 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh[(i / 3) * 4 + i % 3];
+            for (int i = tid; i < L.n_cached; i += kBlockThreads)
+                lds_idx[i] = *reinterpret_cast<const int2*>(p.bvh + 4 * i + 3);
+        }
         __syncthreads();
     }
 #endif
@@ -1020,7 +1079,9 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
     };
     if (item < pool) start();
 
+    VR_T0(t_kernel);
     for (;;) {
+        VR_T0(t_setup);
         if (state == LS_SETUP) {
             if (intersect_spheres<false, FEAT>(p, ray, hr, cnt)) {
                 trav_init<FEAT>(p, ray, hr.t, tr, L);
@@ -1029,6 +1090,8 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
                 state = LS_SHADE;
             }
         }
+        VR_T1(t_setup, 0);
+        VR_T0(t_trav);
         if (HAS(F_MESH)) {
             for (;;) {
                 const int n_trav = __popcll(__ballot(state == LS_TRAV));
@@ -1049,6 +1112,118 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
                 }
             }
         }
+        VR_T1(t_trav, 1);
+        VR_T0(t_shblk);
+        bool ended = false;
+        if (state == LS_SHADE) {
+            VR_LANE(4, 5);
+            vr4 out;
+            if (bounce_step<false, FEAT>(p, ray, hr, ps, out, cnt)) {
+                out_base[(size_t)(q0 + (item >> 6)) * p.path_stride + (item & 63u)] = out;
+                ended = true;
+            } else {
+                state = LS_SETUP;
+            }
+        }
+        VR_T1(t_shblk, 4);
+        const unsigned long long em = __ballot(ended);
+        if (em != 0ull) {
+            if (ended) {
+                item = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                if (item < pool) start();
+                else state = LS_DONE;
+            }
+            next += (uint32_t)__popcll(em);
+        }
+        if (__ballot(state != LS_DONE) == 0ull) break;
+    }
+    VR_T1(t_kernel, 5);
+#if defined(VR_LANESTATS) || defined(VR_TIMING)
+    if (p.counters) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            unsigned long long v = cnt.tm[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+            if (lane == 0) atomicAdd(p.counters + 8 + k, v);
+        }
+    }
+#endif
+}
+
+// Block-queue variant of the path-pool kernel.  Each round, every lane
+// shades its path's last hit and produces its next ray (lanes whose path
+// ended take the next item of their wave's pool); rays that must traverse
+// the mesh are pushed into a block-wide LDS queue, and then all 256 lanes of
+// the block traverse the queued rays together, each lane taking the next
+// queued ray whenever its current one is done.  The traversal no longer runs
+// at the pace of the few deep rays in one wave: it is compacted over the
+// block, and lanes with no path left still traverse other lanes' rays.
+// Results go back through the queue slots.  Every path's operations are
+// unchanged (results bit-identical).
+constexpr int kQueueBytes = 2 * 16 * kBlockThreads + 16;
+
+template <int STACK, uint32_t FEAT>
+__global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_block_kernel(const RenderParams p)
+{
+    constexpr int CN = cache_nodes(STACK, kQueueBytes);
+    __shared__ int lds_stack[STACK * kBlockThreads];
+    __shared__ vr4 lds_nodes[3 * CN];
+    __shared__ int2 lds_idx[CN];
+    __shared__ vr4 q_a[kBlockThreads];                     // (o.xyz, t0) in; (t, bu, bv, best) out
+    __shared__ vr4 q_b[kBlockThreads];                     // (d.xyz, -)
+    __shared__ int q_count, q_next;
+    const int tid = threadIdx.x;
+    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
+    const uint32_t T = p.split;
+    const uint32_t tile = blockIdx.x / T;
+    const uint32_t g = blockIdx.x - tile * T;
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t x0 = tile_x * 16u + (uint32_t)((wave & 1) * 8);
+    const uint32_t y0 = tile_y * 16u + (uint32_t)((wave >> 1) * 8);
+    const uint32_t n_paths = 2u * p.n_frames;
+    const uint32_t chunk = (n_paths + T - 1u) / T;
+    const uint32_t q0 = g * chunk < n_paths ? g * chunk : n_paths;
+    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
+    const uint32_t pool = 64u * (q1 - q0);
+    vr4* const out_base = p.paths + (size_t)tile * kBlockThreads + (size_t)wave * 64u;
+    Cnt cnt;
+
+    uint32_t item = (uint32_t)lane;
+    uint32_t next = 64u;                                   // wave-uniform: first unassigned item
+    int state = LS_DONE;
+    int my_e = 0;                                          // queue slot of this lane's ray
+    Ray ray;
+    PathState ps;
+    HitRec hr;
+    auto start = [&]() {                                   // render's per-sample prologue (:817-844)
+        const uint32_t px = item & 63u, q = q0 + (item >> 6), f = q >> 1;
+        const uint32_t x = x0 + (px & 7u), y = y0 + (px >> 3);
+        uint32_t s1 = x * (p.first_frame + f);
+        uint32_t s2 = y * p.times[f];
+        if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
+        path_begin(ps, s1, s2);
+        ray = camera_ray(p, x, y);
+        state = LS_SETUP;
+    };
+    if (item < pool) start();
+    if (tid == 0) { q_count = 0; q_next = 0; }
+    __syncthreads();
+
+    VR_T0(t_kernel);
+    for (;;) {
+        // results of the last traversal round
+        if (state == LS_TRAV) {
+            const vr4 res = q_a[my_e];
+            const int best = __float_as_int(res.w);
+            if (best >= 0) { hr.t = res.x; hr.kind = HK_MESH; hr.idx = best; hr.bu = res.y; hr.bv = res.z; }
+            state = LS_SHADE;
+        }
+        VR_T0(t_shblk);
         bool ended = false;
         if (state == LS_SHADE) {
             VR_LANE(4, 5);
@@ -1070,9 +1245,73 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
             }
             next += (uint32_t)__popcll(em);
         }
-        if (__ballot(state != LS_DONE) == 0ull) break;
+        VR_T1(t_shblk, 4);
+        VR_T0(t_setup);
+        VR_T0(t_b1);
+        __syncthreads();                                   // every result read: queue slots are free
+        VR_T1(t_b1, 2);
+        if (state == LS_SETUP) {
+            if (intersect_spheres<false, FEAT>(p, ray, hr, cnt)) {
+                my_e = atomicAdd(&q_count, 1);
+                q_a[my_e] = mk4(ray.o.x, ray.o.y, ray.o.z, hr.t);
+                q_b[my_e] = mk4(ray.d.x, ray.d.y, ray.d.z, 0.f);
+                state = LS_TRAV;
+            } else {
+                state = LS_SHADE;
+            }
+        }
+        VR_T1(t_setup, 0);
+        VR_T0(t_b2);
+        const int alive = __syncthreads_or(state != LS_DONE);
+        VR_T1(t_b2, 2);
+        if (!alive) break;
+        VR_T0(t_trav);
+        const int n_q = q_count;
+        if (n_q > 0) {
+            // cooperative traversal of the queued rays
+            bool has = false, exhausted = false;
+            int e = 0;
+            Ray r;
+            Trav tr;
+            for (;;) {
+                if (!exhausted) {
+                    const unsigned long long need = __ballot(!has);
+                    if (need != 0ull) {
+                        int base = 0;
+                        if (lane == __ffsll((long long)need) - 1) base = atomicAdd(&q_next, __popcll(need));
+                        base = __shfl(base, __ffsll((long long)need) - 1, 64);
+                        if (base + __popcll(need) >= n_q) exhausted = true;
+                        if (!has) {
+                            e = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                            if (e < n_q) {
+                                const vr4 a = q_a[e], b = q_b[e];
+                                r.o = mk4(a.x, a.y, a.z, 0.f);
+                                r.d = mk4(b.x, b.y, b.z, 0.f);
+                                trav_init<FEAT>(p, r, a.w, tr, L);
+                                has = true;
+                            }
+                        }
+                    }
+                }
+                if (__ballot(has) == 0ull) break;
+                if (has) {
+                    trav_iter<STACK, false, FEAT>(p, r, tr, L, cnt);
+                    if (tr.nodeAddr == kSentinel) {
+                        q_a[e] = mk4(tr.t, tr.bu, tr.bv, __int_as_float(tr.best));
+                        has = false;
+                    }
+                }
+            }
+        }
+        VR_T1(t_trav, 1);
+        VR_T0(t_b3);
+        __syncthreads();                                   // every result written
+        VR_T1(t_b3, 2);
+        if (tid == 0) { q_count = 0; q_next = 0; }         // read only after the next barrier
     }
-#ifdef VR_LANESTATS
+    VR_T1(t_kernel, 5);
+#if defined(VR_LANESTATS) || defined(VR_TIMING)
     if (p.counters) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
@@ -1158,10 +1397,17 @@ static void launch_spec(const RenderParams& p, uint32_t blocks, int stack_depth,
 #endif
     if (!wave)
         hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+#ifdef VR_BLOCK_QUEUE
+    else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
+        hipLaunchKernelGGL((render_block_kernel<16, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL((render_block_kernel<32, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+#else
     else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
         hipLaunchKernelGGL((render_wave_kernel<16, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
     else
         hipLaunchKernelGGL((render_wave_kernel<32, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+#endif
 }
 
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream)

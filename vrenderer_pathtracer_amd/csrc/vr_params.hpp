@@ -44,6 +44,7 @@ struct RenderParams {
     uint32_t path_stride;            // owned tiles * 256 (scratch row length)
     vr4* paths;                      // per-path results [2*n_frames][path_stride]
     const vr4* bvh;
+    const vr4* bvh16;                // same nodes, conservative fp16 boxes, 32 B each (culled traversal)
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
     const vr3* verts;                // 3 vertices per triangle, compact leaf order
     uint32_t n_tris;                 // triangles in verts/normals/tangents/uvs

@@ -59,7 +59,7 @@ struct vrhip_ctx {
     bool cornell = false, example = false, view_brdf = false;
     bool strict = false;          // exact reference traversal (no t-culling)
     // mesh
-    vr4* bvh = nullptr; vr3* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
+    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr3* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
     uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0;
     bool mesh = false;
@@ -121,6 +121,7 @@ uint32_t owned_tiles_of(uint32_t W, uint32_t H, uint32_t rank, uint32_t n_ranks)
 // leaf tests, and their order, are exactly the reference's.
 struct DeviceMesh {
     std::vector<vr4> nodes, normals, tangents;
+    std::vector<vr4> nodes16;        // 2 x 16 B per node: conservative fp16 boxes + child indices
     std::vector<vr3> tris;           // packed 12 B vertices (vertex .w never reaches a result)
     std::vector<vr2> uvs;
 };
@@ -174,6 +175,65 @@ void order_nodes_by_area(DeviceMesh& dm)
     dm.nodes.swap(out);
 }
 
+// IEEE binary16 bits of x rounded toward -inf (down) or +inf (up), so the
+// half box always contains the float box.  Out-of-range values become
+// -inf / +inf on the outward side.
+uint16_t half_bits_directed(float x, bool up)
+{
+    uint32_t u;
+    std::memcpy(&u, &x, 4);
+    const uint32_t sign = (u >> 16) & 0x8000u;
+    const float ax = std::fabs(x);
+    auto half_to_float = [](uint16_t h) {
+        const uint32_t s = (h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+        float f;
+        if (e == 0) f = std::ldexp((float)m, -24);
+        else if (e == 31) f = m ? NAN : INFINITY;
+        else f = std::ldexp((float)(m | 0x400u), (int)e - 25);
+        return s ? -f : f;
+    };
+    // truncation toward zero of |x| to half precision
+    uint16_t mag;
+    if (ax >= 65504.f) {
+        mag = 0x7bffu;                                   // max finite
+    } else if (ax < std::ldexp(1.f, -14)) {
+        mag = (uint16_t)(ax / std::ldexp(1.f, -24));     // subnormal, truncated
+    } else {
+        int e;
+        const float m = std::frexp(ax, &e);              // ax = m * 2^e, m in [0.5, 1)
+        const uint32_t mant = (uint32_t)std::ldexp(m, 11) & 0x3ffu;   // 10 fraction bits, truncated
+        mag = (uint16_t)(((uint32_t)(e - 1 + 15) << 10) | mant);
+    }
+    uint16_t h = (uint16_t)(sign | mag);
+    // truncation moved |x| toward zero; step one ulp outward where needed
+    const float hv = half_to_float(h);
+    const bool below = hv < x, above = hv > x;
+    if (up && below) h = sign ? (uint16_t)(h - 1) : (uint16_t)(h + 1);
+    if (!up && above) h = sign ? (uint16_t)(h + 1) : (uint16_t)(h - 1);
+    if ((h & 0x7fffu) == 0x7c00u || ((h & 0x7fffu) > 0x7c00u)) h = (uint16_t)((h & 0x8000u) | 0x7c00u);
+    if (up && ax >= 65504.f && x > 0.f && half_to_float(h) < x) h = 0x7c00u;          // +inf
+    if (!up && ax >= 65504.f && x < 0.f && half_to_float(h) > x) h = 0xfc00u;         // -inf
+    return h;
+}
+
+// fp16 copy of the node array for the t-culled traversal: per node
+// [c0.lo.x c0.hi.x c0.lo.y c0.hi.y c0.lo.z c0.hi.z c1.lo.x c1.hi.x]
+// [c1.lo.y c1.hi.y c1.lo.z c1.hi.z idx0 idx1], lows rounded down and highs up.
+void build_nodes16(DeviceMesh& dm)
+{
+    const size_t n = dm.nodes.size() / 4;
+    dm.nodes16.assign(2 * n, vr4{ 0, 0, 0, 0 });
+    for (size_t i = 0; i < n; ++i) {
+        const vr4 n0 = dm.nodes[4 * i], n1 = dm.nodes[4 * i + 1], nz = dm.nodes[4 * i + 2], ni = dm.nodes[4 * i + 3];
+        const float v[12] = { n0.x, n0.y, n0.z, n0.w, nz.x, nz.y, n1.x, n1.y, n1.z, n1.w, nz.z, nz.w };
+        uint16_t h[16];
+        for (int k = 0; k < 12; ++k) h[k] = half_bits_directed(v[k], (k & 1) != 0);
+        std::memcpy(&h[12], &ni.x, 4);
+        std::memcpy(&h[14], &ni.y, 4);
+        std::memcpy(&dm.nodes16[2 * i], h, 32);
+    }
+}
+
 bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const vr4* normals,
                       const vr4* tangents, const vr2* uvs, DeviceMesh& dm, std::string& why)
 {
@@ -222,6 +282,7 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
 #ifndef VR_NO_AREA_ORDER
     order_nodes_by_area(dm);
 #endif
+    build_nodes16(dm);
     if (dm.tris.empty()) {
         dm.tris.push_back(vr3{ 0, 0, 0 });
         dm.normals.push_back(vr4{ 0, 0, 0, 0 });
@@ -299,7 +360,7 @@ int vrhip_destroy(vrhip_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->accum); dfree(c->rgba); dfree(c->depth);
-    dfree(c->bvh); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
+    dfree(c->bvh); dfree(c->bvh16); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     dfree(c->counters); dfree(c->paths);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -365,6 +426,7 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     int rc = set_device(c); if (rc) return rc;
     const size_t nt = dm.tris.size();
     if ((rc = upload(c, c->bvh, dm.nodes.data(), dm.nodes.size() * 16))) return rc;
+    if ((rc = upload(c, c->bvh16, dm.nodes16.data(), dm.nodes16.size() * 16))) return rc;
     if ((rc = upload(c, c->verts, dm.tris.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->normals, dm.normals.data(), nt * 16))) return rc;
     if ((rc = upload(c, c->tangents, dm.tangents.data(), nt * 16))) return rc;
@@ -512,7 +574,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.flags = f;
     p.tiles_x = p.wr / 16u;
     p.rank = c->rank; p.nranks = c->nranks;
-    p.bvh = c->bvh; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
+    p.bvh = c->bvh; p.bvh16 = c->bvh16; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
     p.hdr = c->hdr; p.hdr_w = c->hdr_w; p.hdr_h = c->hdr_h;
     for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
     p.brdf = c->brdf;
