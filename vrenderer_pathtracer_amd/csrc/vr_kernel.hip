@@ -203,6 +203,16 @@ __device__ __forceinline__ int2 buf_load2i(__amdgpu_buffer_rsrc_t b, int off) {
     return make_int2((int)v.x, (int)v.y);
 }
 
+// Conservative fp16 node boxes for the culled traversal (-DVR_FP16_NODES):
+// half the node bytes, but the looser boxes change the visit order, and on
+// C5 one pixel in 8.3 M differed from the strict traversal (fp32 culled: 0),
+// for at most +1.3 % (C3); off by default.
+#ifdef VR_FP16_NODES
+constexpr bool kFp16Nodes = true;
+#else
+constexpr bool kFp16Nodes = false;
+#endif
+
 struct Lds {
     int* stk;                 // this thread's column of the stack
     const vr4* nodes;         // fp32 nodes: 3 rows per cached node; fp16 nodes: 2 rows per node
@@ -279,7 +289,7 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     // wave-uniform choice between the LDS copy and L2/HBM: a diverged wave
     // would pay both round trips
     const bool in_lds = __ballot(node >= L.n_cached) == 0ull;
-    if (!strict) {
+    if (kFp16Nodes && !strict) {
         // conservative fp16 boxes (lows rounded down, highs up): two 16-B
         // fetches per node instead of four; a box can only grow, so no hit
         // the exact box admits is lost
@@ -890,7 +900,7 @@ __device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, 
     L.n_cached = 0;
 #ifndef VR_NO_NODE_CACHE
     if (HAS(F_MESH)) {
-        if (!HAS(F_STRICT)) {                          // fp16 nodes, 32 B: 1.5x as many fit
+        if (kFp16Nodes && !HAS(F_STRICT)) {            // fp16 nodes, 32 B: 1.5x as many fit
             const uint32_t cap = (uint32_t)(3 * cn / 2);
             L.n_cached = (int)(p.n_nodes < cap ? p.n_nodes : cap);
             for (int i = tid; i < 2 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh16[i];

@@ -92,6 +92,8 @@ class TileGather:
         if self.world == 1:
             return
         own_stream = self.r.get_stream() != torch.cuda.current_stream(self.device).cuda_stream
+        if own_stream:
+            torch.cuda.current_stream(self.device).synchronize()   # the last collective has read `send`
         self.r.pack_tiles(self.what, self.send.data_ptr())
         if own_stream or self.host:
             self.r.sync()                     # the collective reads `send` on torch's stream
