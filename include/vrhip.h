@@ -113,6 +113,24 @@ int vrhip_upload_texture(vrhip_ctx *ctx, int type, const float *rgba, uint32_t w
  * reproduces the reference's delete[]). */
 int vrhip_upload_brdf(vrhip_ctx *ctx, const float *table, size_t n_floats);
 
+/* replaces vBRDFLoader::loadBinary (src/BRDFLoader.cpp:15-50): reads a MERL
+ * .binary file (3 int32 dims, then 3*90*90*180 doubles, planar R,G,B) into
+ * `table` as floats in the same order.  Host only; the caller passes the
+ * table to vrhip_upload_brdf.  VRHIP_ERR_INVALID on a dimension mismatch or
+ * short file (the reference prints and returns nullptr). */
+int vrhip_load_merl(const char *path, float *table, size_t n_floats);
+
+/* ---- display interop ---------------------------------------------------- */
+/* replaces vRendererCuda::registerTextureBuffer / registerDepthBuffer
+ * (src/vRendererCuda.cpp:57-67): registers an OpenGL texture (which = 0:
+ * colour, 1: depth; target e.g. GL_TEXTURE_2D = 0x0DE1) with HIP.  Needs the
+ * caller's GL context current. */
+int vrhip_gl_register_image(vrhip_ctx *ctx, int which, unsigned int gl_texture, unsigned int gl_target);
+/* Copies the RGBA8 colour and depth images into the registered textures
+ * (map, device-to-array copy, unmap); the reference's kernel wrote them
+ * through surfaces (src/vRendererCuda.cpp:117-162). Synchronous. */
+int vrhip_gl_present(vrhip_ctx *ctx);
+
 /* ---- rendering -------------------------------------------------------- */
 /* replaces vRendererCuda::render (src/vRendererCuda.cpp:107-165) +
  * cu_runRenderKernel (cuda/src/PathTracer.cu:870-892), for n_frames

@@ -20,6 +20,8 @@ vRendererHIP::vRendererHIP() :
   m_ctx(nullptr),
   m_texture(0),
   m_depthTexture(0),
+  m_interopTexture(false),
+  m_interopDepth(false),
   m_hasTexture(false),
   m_hasDepth(false),
   m_width(0),
@@ -62,16 +64,21 @@ void vRendererHIP::init(const unsigned int &_w, const unsigned int &_h)
   m_initialised = true;
 }
 
+// GL interop first (HIP maps the texture; the frame is copied device to
+// device), read-back + glTexSubImage2D when the driver refuses interop
+// (e.g. a GL context on another device).
 void vRendererHIP::registerTextureBuffer(GLuint &_texture)
 {
   m_texture = _texture;
   m_hasTexture = true;
+  m_interopTexture = vrhip_gl_register_image(m_ctx, 0, _texture, GL_TEXTURE_2D) == VRHIP_OK;
 }
 
 void vRendererHIP::registerDepthBuffer(GLuint &_depthTexture)
 {
   m_depthTexture = _depthTexture;
   m_hasDepth = true;
+  m_interopDepth = vrhip_gl_register_image(m_ctx, 1, _depthTexture, GL_TEXTURE_2D) == VRHIP_OK;
 }
 
 void vRendererHIP::updateCamera()
@@ -113,13 +120,15 @@ void vRendererHIP::render()
   validate(vrhip_render(m_ctx, 1, nullptr, t), "Render");
   validate(vrhip_sync(m_ctx), "Synchronize");
 
-  if(m_hasTexture)
+  if(m_interopTexture || m_interopDepth)
+    validate(vrhip_gl_present(m_ctx), "Present to GL");
+  if(m_hasTexture && !m_interopTexture)
   {
     validate(vrhip_read_rgba8(m_ctx, m_rgba.data()), "Read colour buffer");
     glBindTexture(GL_TEXTURE_2D, m_texture);
     glTexSubImage2D(GL_TEXTURE_2D, 0, 0, 0, m_width, m_height, GL_RGBA, GL_UNSIGNED_BYTE, m_rgba.data());
   }
-  if(m_hasDepth)
+  if(m_hasDepth && !m_interopDepth)
   {
     validate(vrhip_read_depth8(m_ctx, m_depth.data()), "Read depth buffer");
     glBindTexture(GL_TEXTURE_2D, m_depthTexture);

@@ -47,6 +47,8 @@ private:
   vrhip_ctx *m_ctx;
   GLuint m_texture;
   GLuint m_depthTexture;
+  bool m_interopTexture;
+  bool m_interopDepth;
   bool m_hasTexture;
   bool m_hasDepth;
   std::vector<unsigned char> m_rgba;

@@ -9,7 +9,7 @@ SRC="vrenderer_pathtracer_amd/csrc/vr_kernel.hip vrenderer_pathtracer_amd/csrc/v
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
   ( rm -f variants/libvrhip_$name.so
-    hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -shared --offload-arch=gfx950 $flags \
+    hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -shared -pthread --offload-arch=gfx950 $flags \
       -o variants/libvrhip_$name.so $SRC -Rpass-analysis=kernel-resource-usage > variants/$name.log 2>&1
     grep -E -A12 "render_(wave|block)_kernelILi..ELj9E" variants/$name.log | grep -E "VGPRs:|VGPRs Spill|Scratch" \
       | sed 's/.*remark: *//;s/ \[-Rpass.*//' | tr '\n' ' ' | sed "s/^/$name: /"; echo

@@ -5,6 +5,7 @@ declared symbol, fail loudly (status codes, no exit) without a device, and
 its host helpers (BVH build, flattening, validation, tiling) must be right.
 """
 import ctypes
+import os
 import re
 import subprocess
 
@@ -17,6 +18,7 @@ from vrenderer_pathtracer_amd.build import LIB_PATH
 from vrenderer_pathtracer_amd.tiles import owned_pixels, pack_host, unpack_host
 
 _f = ctypes.POINTER(ctypes.c_float)
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_library_exports_every_header_symbol(native):
@@ -176,3 +178,46 @@ def test_pack_unpack_host_roundtrip(native):
     out = np.zeros_like(img)
     unpack_host(packed, out)
     assert np.array_equal(out, img)
+
+
+def test_parallel_builder_is_deterministic(native):
+    """The multi-threaded SAH builder (vr_bvh.cpp) gives the same flattened tree
+    for any thread count (min/max boxes and counts are order-independent)."""
+    import subprocess
+    import sys
+    code = ("import hashlib, sys; sys.path.insert(0, %r)\n"
+            "from vrenderer_pathtracer_amd import scenes, renderer\n"
+            "f = renderer.build_flat(scenes.torus_knot(400, 200))\n"
+            "print(hashlib.sha1(b''.join(f[k].tobytes() for k in sorted(f))).hexdigest())\n") % REPO
+    hashes = set()
+    for threads in ("1", "3", "8"):
+        env = dict(os.environ, VRHIP_BUILD_THREADS=threads)
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr[-2000:]
+        hashes.add(out.stdout.strip())
+    assert len(hashes) == 1
+
+
+def test_load_merl_matches_reference_layout(native, tmp_path):
+    """vrhip_load_merl == vBRDFLoader::loadBinary: dims header, doubles -> floats, same order."""
+    from vrenderer_pathtracer_amd.renderer import load_merl
+    n = 90 * 90 * 180
+    vals = np.random.default_rng(3).random(3 * n) * 3.0
+    f = tmp_path / "test.binary"
+    with open(f, "wb") as fh:
+        fh.write(np.array([90, 90, 180], np.int32).tobytes())
+        fh.write(vals.astype(np.float64).tobytes())
+    got = load_merl(f)
+    assert np.array_equal(got, vals.astype(np.float32))
+    bad = tmp_path / "bad.binary"
+    with open(bad, "wb") as fh:
+        fh.write(np.array([90, 90, 90], np.int32).tobytes())
+        fh.write(vals[: 3 * 90 * 90 * 90].astype(np.float64).tobytes())
+    with pytest.raises(_native.VRHIPError):
+        load_merl(bad)
+    short = tmp_path / "short.binary"
+    with open(short, "wb") as fh:
+        fh.write(np.array([90, 90, 180], np.int32).tobytes())
+        fh.write(vals[:1000].astype(np.float64).tobytes())
+    with pytest.raises(_native.VRHIPError):
+        load_merl(short)

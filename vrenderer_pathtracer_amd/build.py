@@ -20,7 +20,7 @@ ARCH = os.environ.get("VRHIP_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: results are defined without FMA contraction (parity
 # with the CPU oracle); division and sqrt stay IEEE (hipcc default).
-HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
+HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", "-pthread",
                f"--offload-arch={ARCH}"]
 
 

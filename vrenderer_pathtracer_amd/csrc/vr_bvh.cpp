@@ -15,6 +15,9 @@
 #include "vr_bvh.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <thread>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -57,7 +60,9 @@ struct Builder {
     std::vector<Box> tri_box;
     std::vector<float> centroid;       // 3 per triangle
     std::vector<uint32_t> refs;        // triangle references (leaf ranges index this)
-    std::vector<BuildNode> nodes;
+    std::vector<BuildNode> nodes;      // preallocated; slots taken with an atomic counter
+    std::atomic<uint32_t> n_nodes{ 0 };
+    std::atomic<int> spare_threads{ 0 };
 
 #ifndef VR_BVH_BINS
 #define VR_BVH_BINS 128
@@ -66,49 +71,102 @@ struct Builder {
 #define VR_BVH_NODE_COST 1.0
 #endif
     static constexpr int kBins = VR_BVH_BINS;
+    static constexpr uint32_t kParallelTask = 16384;    // subtrees at least this big may get a thread
+    static constexpr uint32_t kParallelBin = 131072;    // nodes at least this big bin in parallel
 
+    int store(const BuildNode& n) {
+        const uint32_t i = n_nodes.fetch_add(1);
+        nodes[i] = n;
+        return (int)i;
+    }
     int make_leaf(uint32_t first, uint32_t count, const Box& b) {
         BuildNode n; n.box = b; n.first = first; n.count = count; n.leaf = true;
-        nodes.push_back(n);
-        return (int)nodes.size() - 1;
+        return store(n);
     }
 
-    // Returns node index.  force_split: the root must be an inner node (the
-    // flattened layout stores leaves inside their parent).
-    int build(uint32_t first, uint32_t count, uint32_t depth, bool force_split) {
-        Box b, cb;
+    // bounds and centroid bounds of refs[first, first+count)
+    void bounds(uint32_t first, uint32_t count, Box& b, Box& cb) const {
         for (uint32_t i = first; i < first + count; ++i) {
             b.grow(tri_box[refs[i]]);
             cb.grow(&centroid[3 * refs[i]]);
         }
-        if (!force_split && (count <= 1 || depth + 1 >= max_depth)) return make_leaf(first, count, b);
-
-        // binned SAH over centroids
-        double best_cost = std::numeric_limits<double>::infinity();
-        int best_axis = -1, best_split = -1;
+    }
+    struct Bins {
+        Box box[3][kBins];
+        uint32_t cnt[3][kBins] = {};
+    };
+    void bin(uint32_t first, uint32_t count, const Box& cb, Bins& out) const {
         for (int a = 0; a < 3; ++a) {
             const float ext = cb.hi[a] - cb.lo[a];
             if (!(ext > 0.f)) continue;
-            Box bin_box[kBins];
-            uint32_t bin_cnt[kBins] = {};
             const double scale = kBins / (double)ext;
             for (uint32_t i = first; i < first + count; ++i) {
                 const uint32_t t = refs[i];
                 int k = (int)(((double)centroid[3 * t + a] - cb.lo[a]) * scale);
                 k = std::min(std::max(k, 0), kBins - 1);
-                bin_cnt[k]++;
-                bin_box[k].grow(tri_box[t]);
+                out.cnt[a][k]++;
+                out.box[a][k].grow(tri_box[t]);
             }
+        }
+    }
+    // Runs f(chunk_first, chunk_count, chunk_index) over `parts` chunks on threads.
+    template <typename F>
+    static void parallel_chunks(uint32_t first, uint32_t count, int parts, F f) {
+        std::vector<std::thread> th;
+        const uint32_t step = (count + parts - 1) / parts;
+        for (int c = 0; c < parts; ++c) {
+            const uint32_t f0 = first + c * step;
+            if (f0 >= first + count) break;
+            const uint32_t n = std::min(step, first + count - f0);
+            th.emplace_back(f, f0, n, c);
+        }
+        for (auto& t : th) t.join();
+    }
+
+    // Returns node index.  force_split: the root must be an inner node (the
+    // flattened layout stores leaves inside their parent).  Min/max boxes and
+    // counts are order-independent, so the tree does not depend on threading.
+    int build(uint32_t first, uint32_t count, uint32_t depth, bool force_split) {
+        Box b, cb;
+        Bins bins;
+        const int par = count >= kParallelBin ? std::max(1, std::min(spare_threads.load() + 1, 16)) : 1;
+        if (par > 1) {
+            std::vector<Box> pb(par), pcb(par);
+            parallel_chunks(first, count, par, [&](uint32_t f0, uint32_t n, int c) { bounds(f0, n, pb[c], pcb[c]); });
+            for (int c = 0; c < par; ++c) { b.grow(pb[c]); cb.grow(pcb[c]); }
+        } else {
+            bounds(first, count, b, cb);
+        }
+        if (!force_split && (count <= 1 || depth + 1 >= max_depth)) return make_leaf(first, count, b);
+
+        // binned SAH over centroids
+        if (par > 1) {
+            std::vector<Bins> pbins(par);
+            parallel_chunks(first, count, par, [&](uint32_t f0, uint32_t n, int c) { bin(f0, n, cb, pbins[c]); });
+            for (int c = 0; c < par; ++c)
+                for (int a = 0; a < 3; ++a)
+                    for (int k = 0; k < kBins; ++k) {
+                        bins.cnt[a][k] += pbins[c].cnt[a][k];
+                        bins.box[a][k].grow(pbins[c].box[a][k]);
+                    }
+        } else {
+            bin(first, count, cb, bins);
+        }
+        double best_cost = std::numeric_limits<double>::infinity();
+        int best_axis = -1, best_split = -1;
+        for (int a = 0; a < 3; ++a) {
+            const float ext = cb.hi[a] - cb.lo[a];
+            if (!(ext > 0.f)) continue;
             double right_area[kBins];
             uint32_t right_cnt[kBins];
             Box acc; uint32_t c = 0;
             for (int k = kBins - 1; k > 0; --k) {
-                acc.grow(bin_box[k]); c += bin_cnt[k];
+                acc.grow(bins.box[a][k]); c += bins.cnt[a][k];
                 right_area[k] = acc.area(); right_cnt[k] = c;
             }
             acc = Box(); c = 0;
             for (int k = 0; k < kBins - 1; ++k) {
-                acc.grow(bin_box[k]); c += bin_cnt[k];
+                acc.grow(bins.box[a][k]); c += bins.cnt[a][k];
                 if (c == 0 || right_cnt[k + 1] == 0) continue;
                 const double cost = acc.area() * c + right_area[k + 1] * right_cnt[k + 1];
                 if (cost < best_cost) { best_cost = cost; best_axis = a; best_split = k; }
@@ -141,15 +199,34 @@ struct Builder {
             // (the second test ties at equal t and the strict < keeps the first)
             left = make_leaf(first, 1, b);
             right = make_leaf(first, 1, b);
+        } else if (mid - first >= kParallelTask && first + count - mid >= kParallelTask &&
+                   spare_threads.fetch_sub(1) > 0) {
+            std::thread t([&] { left = build(first, mid - first, depth + 1, false); });
+            right = build(mid, first + count - mid, depth + 1, false);
+            t.join();
+            spare_threads.fetch_add(1);
         } else {
+            if (mid - first >= kParallelTask && first + count - mid >= kParallelTask) spare_threads.fetch_add(1);
             left = build(first, mid - first, depth + 1, false);
             right = build(mid, first + count - mid, depth + 1, false);
         }
         BuildNode n; n.box = b; n.child[0] = left; n.child[1] = right; n.leaf = false;
-        nodes.push_back(n);
-        return (int)nodes.size() - 1;
+        return store(n);
     }
 };
+
+// Host threads for the builder: VRHIP_BUILD_THREADS, else OMP_NUM_THREADS,
+// else the machine's concurrency, at most 16.
+int build_threads()
+{
+    int n = 0;
+    for (const char* var : { "VRHIP_BUILD_THREADS", "OMP_NUM_THREADS" }) {
+        const char* v = std::getenv(var);
+        if (v && std::atoi(v) > 0) { n = std::atoi(v); break; }
+    }
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(n, 16));
+}
 
 inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 inline int32_t fbits(float f) { int32_t i; std::memcpy(&i, &f, 4); return i; }
@@ -182,7 +259,8 @@ int build_flat(const float* positions, const float* normals, const float* tangen
         for (int a = 0; a < 3; ++a) B.centroid[3 * (size_t)t + a] = 0.5f * (bx.lo[a] + bx.hi[a]);
         B.refs[t] = t;
     }
-    B.nodes.reserve(2 * (size_t)n_tris + 2);
+    B.nodes.resize(2 * (size_t)n_tris + 2);
+    B.spare_threads = build_threads() - 1;
     const int root = B.build(0, n_tris, 0, true);
 
     // Flatten (reference: explicit-stack DFS, src/vRendererCuda.cpp:204-279)

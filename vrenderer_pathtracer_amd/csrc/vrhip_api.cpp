@@ -7,10 +7,12 @@
 // passed by value in the launch instead of __constant__ symbol copies
 // (cuda/src/PathTracer.cu:976-1001), and multi-frame render steps.
 #include <hip/hip_runtime.h>
+#include <hip/hip_gl_interop.h>
 
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <queue>
 #include <string>
 #include <unordered_map>
@@ -83,6 +85,8 @@ struct vrhip_ctx {
     double kernel_ms_total = 0.0;
     uint64_t launches_total = 0, launches_pending = 0;
     unsigned long long* counters = nullptr;
+    // GL interop (colour, depth textures registered by the display host)
+    hipGraphicsResource_t gl_res[2] = { nullptr, nullptr };
 };
 
 namespace {
@@ -362,6 +366,8 @@ int vrhip_destroy(vrhip_ctx* c)
     dfree(c->accum); dfree(c->rgba); dfree(c->depth);
     dfree(c->bvh); dfree(c->bvh16); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
+    for (int i = 0; i < 2; ++i)
+        if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
     dfree(c->counters); dfree(c->paths);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -496,6 +502,53 @@ int vrhip_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
     if (!c || !table || n_floats != 3 * n) return fail(VRHIP_ERR_INVALID, "BRDF table must hold 3*1458000 floats");
     int rc = set_device(c); if (rc) return rc;
     if ((rc = upload(c, c->brdf, table, 3 * n * sizeof(float)))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return VRHIP_OK;
+}
+
+int vrhip_load_merl(const char* path, float* table, size_t n_floats)
+{
+    const size_t n = 90u * 90u * 360u / 2u;
+    if (!path || !table || n_floats != 3 * n) return fail(VRHIP_ERR_INVALID, "BRDF table must hold 3*1458000 floats");
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return fail(VRHIP_ERR_INVALID, std::string("cannot open ") + path);
+    int32_t dims[3] = { 0, 0, 0 };
+    f.read(reinterpret_cast<char*>(dims), sizeof(dims));
+    if (!f || (size_t)dims[0] * (size_t)dims[1] * (size_t)dims[2] != n)
+        return fail(VRHIP_ERR_INVALID, "MERL dimensions don't match 90x90x180");
+    std::vector<double> d(3 * n);
+    f.read(reinterpret_cast<char*>(d.data()), (std::streamsize)(3 * n * sizeof(double)));
+    if (!f) return fail(VRHIP_ERR_INVALID, "truncated MERL file");
+    for (size_t i = 0; i < 3 * n; ++i) table[i] = (float)d[i];
+    return VRHIP_OK;
+}
+
+int vrhip_gl_register_image(vrhip_ctx* c, int which, unsigned int gl_texture, unsigned int gl_target)
+{
+    if (!c || which < 0 || which > 1) return fail(VRHIP_ERR_INVALID, "bad GL registration arguments");
+    int rc = set_device(c); if (rc) return rc;
+    if (c->gl_res[which]) { HIP_TRY(hipGraphicsUnregisterResource(c->gl_res[which])); c->gl_res[which] = nullptr; }
+    HIP_TRY(hipGraphicsGLRegisterImage(&c->gl_res[which], gl_texture, gl_target, hipGraphicsRegisterFlagsWriteDiscard));
+    return VRHIP_OK;
+}
+
+int vrhip_gl_present(vrhip_ctx* c)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    int rc = set_device(c); if (rc) return rc;
+    const void* src[2] = { c->rgba, c->depth };
+    for (int i = 0; i < 2; ++i) {
+        if (!c->gl_res[i]) continue;
+        hipArray_t arr = nullptr;
+        HIP_TRY(hipGraphicsMapResources(1, &c->gl_res[i], c->stream));
+        hipError_t e = hipGraphicsSubResourceGetMappedArray(&arr, c->gl_res[i], 0, 0);
+        if (e == hipSuccess)
+            e = hipMemcpy2DToArrayAsync(arr, 0, 0, src[i], (size_t)c->W * 4, (size_t)c->W * 4, c->H,
+                                        hipMemcpyDeviceToDevice, c->stream);
+        const hipError_t u = hipGraphicsUnmapResources(1, &c->gl_res[i], c->stream);
+        if (e != hipSuccess) return fail(VRHIP_ERR_HIP, std::string("GL present: ") + hipGetErrorString(e));
+        if (u != hipSuccess) return fail(VRHIP_ERR_HIP, std::string("GL unmap: ") + hipGetErrorString(u));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return VRHIP_OK;
 }

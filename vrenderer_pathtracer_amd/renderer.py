@@ -80,6 +80,15 @@ def validate_flat(flat: dict) -> tuple[int, int]:
     return d.value, n.value
 
 
+def load_merl(path: str) -> np.ndarray:
+    """vBRDFLoader::loadBinary (src/BRDFLoader.cpp:15-50) through the C ABI:
+    a MERL .binary file as float32[3*90*90*180] (planar R, G, B), ready for loadBRDF."""
+    L = _native.lib()
+    out = np.zeros(BRDF_TABLE_FLOATS, np.float32)
+    check(L.vrhip_load_merl(str(path).encode(), fptr(out), out.size), "vrhip_load_merl")
+    return out
+
+
 class Camera:
     """Host camera state, the reference's Camera (src/Camera.cpp) reduced to
     what the renderer consumes: origin, dir, up, right, fovScale."""
