@@ -120,8 +120,13 @@ void vRendererHIP::render()
   validate(vrhip_render(m_ctx, 1, nullptr, t), "Render");
   validate(vrhip_sync(m_ctx), "Synchronize");
 
-  if(m_interopTexture || m_interopDepth)
-    validate(vrhip_gl_present(m_ctx), "Present to GL");
+  if((m_interopTexture || m_interopDepth) && vrhip_gl_present(m_ctx) != VRHIP_OK)
+  {
+    // the driver accepted the registration but cannot map it (no shared GL
+    // context): use the read-back path from now on
+    std::cerr << "GL interop unavailable (" << vrhip_last_error() << "), using read-back\n";
+    m_interopTexture = m_interopDepth = false;
+  }
   if(m_hasTexture && !m_interopTexture)
   {
     validate(vrhip_read_rgba8(m_ctx, m_rgba.data()), "Read colour buffer");

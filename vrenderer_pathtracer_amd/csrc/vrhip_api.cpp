@@ -528,7 +528,13 @@ int vrhip_gl_register_image(vrhip_ctx* c, int which, unsigned int gl_texture, un
     if (!c || which < 0 || which > 1) return fail(VRHIP_ERR_INVALID, "bad GL registration arguments");
     int rc = set_device(c); if (rc) return rc;
     if (c->gl_res[which]) { HIP_TRY(hipGraphicsUnregisterResource(c->gl_res[which])); c->gl_res[which] = nullptr; }
-    HIP_TRY(hipGraphicsGLRegisterImage(&c->gl_res[which], gl_texture, gl_target, hipGraphicsRegisterFlagsWriteDiscard));
+    const hipError_t e = hipGraphicsGLRegisterImage(&c->gl_res[which], gl_texture, gl_target,
+                                                    hipGraphicsRegisterFlagsWriteDiscard);
+    if (e != hipSuccess) {
+        c->gl_res[which] = nullptr;
+        (void)hipGetLastError();        // not sticky: later launches check hipGetLastError
+        return fail(VRHIP_ERR_HIP, std::string("hipGraphicsGLRegisterImage: ") + hipGetErrorString(e));
+    }
     return VRHIP_OK;
 }
 
@@ -665,6 +671,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         c->kev.push_back(e);
     }
     c->kev_pairs = 0;
+    (void)hipGetLastError();            // launches below report their own errors only
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     uint32_t done = 0;
     while (done < n_frames) {
