@@ -113,7 +113,7 @@ struct HitRec {
 // Per-lane event counts for the counting variant (algorithmic bytes).
 struct Cnt {
     uint32_t rays = 0, nodes = 0, slots = 0, tris = 0, attr = 0, tex = 0, hdr = 0, brdf = 0;
-#if defined(VR_TIMING) || defined(VR_LANESTATS)
+#if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS)
     // diagnostic builds only.  VR_TIMING: per-lane s_memtime cycles in
     // spheres, mesh traversal, hit materialisation, shading, tonemap, whole
     // kernel.  VR_LANESTATS: active lanes and wave iterations of the node
@@ -288,6 +288,10 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     const int node = tr.nodeAddr >> 2;
     // wave-uniform choice between the LDS copy and L2/HBM: a diverged wave
     // would pay both round trips
+#ifdef VR_NODE_STAMPS
+    uint64_t ns0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns0) :: "memory");
+#endif
     const bool in_lds = __ballot(node >= L.n_cached) == 0ull;
     if (kFp16Nodes && !strict) {
         // conservative fp16 boxes (lows rounded down, highs up): two 16-B
@@ -329,6 +333,13 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
         idx0 = ni.x;
         idx1 = ni.y;
     }
+#ifdef VR_NODE_STAMPS
+    uint64_t ns1;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns1) :: "memory");
+    asm volatile("" ::"v"(n0.x), "v"(n1.x), "v"(nz.x), "v"(idx0), "v"(idx1));
+    cnt.tm[0] += ns1 - ns0;
+    cnt.tm[2] += 1;
+#endif
     // slab distances n*inv - o*inv (:307-322); the culled mode lets
     // them contract to one v_fma each (more accurate)
     auto slab = [&](float n, float iv, float od) {
@@ -361,6 +372,13 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     const bool none = !tc0 && !tc1;
     const int nearc = (both && swp) ? idx1 : (tc0 ? idx0 : idx1);
     const int farc = swp ? idx0 : idx1;
+#ifdef VR_NODE_STAMPS
+    {
+        uint64_t ns2;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns2) :: "memory");
+        cnt.tm[1] += ns2 - ns1;
+    }
+#endif
 #ifdef VR_TOP_IN_REG
     // branch-free, stack top in a register: the entry below the new top is
     // read every visit but only consumed by a later pop
@@ -385,7 +403,11 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
 template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Trav& tr, int k, Cnt& cnt)
 {
+#ifdef VR_DROP_TRIS
+    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, 0u);     // timing probe: loads return 0
+#else
     const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, p.n_tris * 36u);
+#endif
     const bool strict = HAS(F_STRICT);
     if (COUNT) cnt.tris++;
     VR_LANE(2, 3);
@@ -1154,7 +1176,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
         if (__ballot(state != LS_DONE) == 0ull) break;
     }
     VR_T1(t_kernel, 5);
-#if defined(VR_LANESTATS) || defined(VR_TIMING)
+#if defined(VR_LANESTATS) || defined(VR_TIMING) || defined(VR_NODE_STAMPS)
     if (p.counters) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
@@ -1339,6 +1361,125 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_b
 #endif
 }
 
+// Two-paths-per-lane variant of the path-pool kernel (-DVR_TWO_PATHS): each
+// lane holds two paths; it traverses one ray at a time and, when that ray's
+// traversal ends, switches at once to its other path's ray if that one is
+// waiting, so a lane idles in the traversal loop only when both its paths
+// wait for shading.
+enum SlotState : int { SS_SETUP = 0, SS_READY = 1, SS_TRAV = 2, SS_SHADE = 3, SS_DONE = 4 };
+struct Slot {
+    uint32_t item;
+    int st;
+    Ray ray;
+    PathState ps;
+    HitRec hr;
+};
+
+template <int STACK, uint32_t FEAT>
+__global__ void __launch_bounds__(kBlockThreads, 3) render_wave2_kernel(const RenderParams p)
+{
+    constexpr int CN = cache_nodes(STACK);
+    __shared__ int lds_stack[STACK * kBlockThreads];
+    __shared__ vr4 lds_nodes[3 * CN];
+    __shared__ int2 lds_idx[CN];
+    const int tid = threadIdx.x;
+    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
+    const uint32_t T = p.split;
+    const uint32_t tile = blockIdx.x / T;
+    const uint32_t g = blockIdx.x - tile * T;
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint32_t gtile = p.rank + tile * p.nranks;
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t x0 = tile_x * 16u + (uint32_t)((wave & 1) * 8);
+    const uint32_t y0 = tile_y * 16u + (uint32_t)((wave >> 1) * 8);
+    const uint32_t n_paths = 2u * p.n_frames;
+    const uint32_t chunk = (n_paths + T - 1u) / T;
+    const uint32_t q0 = g * chunk < n_paths ? g * chunk : n_paths;
+    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
+    const uint32_t pool = 64u * (q1 - q0);
+    vr4* const out_base = p.paths + (size_t)tile * kBlockThreads + (size_t)wave * 64u;
+    Cnt cnt;
+
+    auto start = [&](Slot& sl) {                           // render's per-sample prologue (:817-844)
+        const uint32_t px = sl.item & 63u, q = q0 + (sl.item >> 6), f = q >> 1;
+        const uint32_t x = x0 + (px & 7u), y = y0 + (px >> 3);
+        uint32_t s1 = x * (p.first_frame + f);
+        uint32_t s2 = y * p.times[f];
+        if (q & 1u) (void)hash_seeds(s1, s2);
+        path_begin(sl.ps, s1, s2);
+        sl.ray = camera_ray(p, x, y);
+        sl.st = SS_SETUP;
+    };
+    auto setup = [&](Slot& sl) {
+        if (sl.st == SS_SETUP)
+            sl.st = intersect_spheres<false, FEAT>(p, sl.ray, sl.hr, cnt) ? SS_READY : SS_SHADE;
+    };
+    Slot sa, sb;
+    sa.item = (uint32_t)lane; sa.st = SS_DONE;
+    sb.item = 64u + (uint32_t)lane; sb.st = SS_DONE;
+    if (sa.item < pool) start(sa);
+    if (sb.item < pool) start(sb);
+    uint32_t next = 128u;                                  // wave-uniform: first unassigned item
+    int cur = -1;                                          // slot being traversed
+    Ray rt;
+    Trav tr;
+    auto try_start = [&]() {
+        if (cur < 0) {
+            if (sa.st == SS_READY) { cur = 0; sa.st = SS_TRAV; rt = sa.ray; trav_init<FEAT>(p, rt, sa.hr.t, tr, L); }
+            else if (sb.st == SS_READY) { cur = 1; sb.st = SS_TRAV; rt = sb.ray; trav_init<FEAT>(p, rt, sb.hr.t, tr, L); }
+        }
+    };
+
+    for (;;) {
+        setup(sa);
+        setup(sb);
+        try_start();
+        for (;;) {
+            const int n_trav = __popcll(__ballot(cur >= 0));
+            if (n_trav == 0) break;
+            const int n_wait = __popcll(__ballot(cur < 0 && (sa.st == SS_SHADE || sb.st == SS_SHADE)));
+            if (n_wait >= VR_SHADE_BATCH && n_wait * VR_SHADE_RATIO >= n_trav) break;
+            if (cur >= 0) {
+                trav_iter<STACK, false, FEAT>(p, rt, tr, L, cnt);
+                if (tr.nodeAddr == kSentinel) {
+                    if (cur == 0) { trav_finish(tr, sa.hr); sa.st = SS_SHADE; }
+                    else { trav_finish(tr, sb.hr); sb.st = SS_SHADE; }
+                    cur = -1;
+                    setup(sa);
+                    setup(sb);
+                    try_start();
+                }
+            }
+        }
+        auto shade = [&](Slot& sl) {
+            bool ended = false;
+            if (sl.st == SS_SHADE) {
+                vr4 out;
+                if (bounce_step<false, FEAT>(p, sl.ray, sl.hr, sl.ps, out, cnt)) {
+                    out_base[(size_t)(q0 + (sl.item >> 6)) * p.path_stride + (sl.item & 63u)] = out;
+                    ended = true;
+                } else {
+                    sl.st = SS_SETUP;
+                }
+            }
+            const unsigned long long em = __ballot(ended);
+            if (em != 0ull) {
+                if (ended) {
+                    sl.item = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                    if (sl.item < pool) start(sl);
+                    else sl.st = SS_DONE;
+                }
+                next += (uint32_t)__popcll(em);
+            }
+        };
+        shade(sa);
+        shade(sb);
+        if (__ballot(sa.st != SS_DONE || sb.st != SS_DONE || cur >= 0) == 0ull) break;
+    }
+}
+
 // ---- small helper kernels ------------------------------------------------
 __global__ void half_to_float_kernel(const uint16_t* __restrict__ src, vr4* __restrict__ dst, size_t n)
 {
@@ -1412,7 +1553,12 @@ static void launch_spec(const RenderParams& p, uint32_t blocks, int stack_depth,
 #endif
     if (!wave)
         hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-#ifdef VR_BLOCK_QUEUE
+#if defined(VR_TWO_PATHS)
+    else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
+        hipLaunchKernelGGL((render_wave2_kernel<16, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL((render_wave2_kernel<32, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+#elif defined(VR_BLOCK_QUEUE)
     else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
         hipLaunchKernelGGL((render_block_kernel<16, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
     else

@@ -137,6 +137,11 @@ constexpr int kLeafCountBits = 7;
 // kernel keeps a prefix of this array in LDS: the boxes a random ray is most
 // likely to enter.  Only addresses change -- every node keeps its boxes and
 // child order, so the traversal visits the same nodes in the same order.
+#ifndef VR_TOP_NODES
+#define VR_TOP_NODES 1024
+#endif
+constexpr size_t kTopNodes = VR_TOP_NODES;    // >= any kernel's LDS node cache
+
 void order_nodes_by_area(DeviceMesh& dm)
 {
     const size_t n = dm.nodes.size() / 4;
@@ -147,23 +152,52 @@ void order_nodes_by_area(DeviceMesh& dm)
         const float dx = a.y - a.x, dy = a.w - a.z, dz = ch ? z.w - z.z : z.y - z.x;
         return dx * dy + dy * dz + dz * dx;
     };
+    auto child = [&](size_t node, int ch) {
+        int32_t idx;
+        std::memcpy(&idx, &dm.nodes[4 * node + 3].x + ch, 4);
+        return idx;
+    };
     std::vector<int32_t> newoff(n, -1);
     std::vector<size_t> order;
     order.reserve(n);
+    // the first kTop nodes: largest boxes first (the LDS-cached prefix)
     std::priority_queue<std::pair<float, int64_t>> pq;   // (area, -node): ties by address
     pq.push({ INFINITY, 0 });
     newoff[0] = 0;
-    while (!pq.empty()) {
+    while (!pq.empty() && order.size() < kTopNodes) {
         const size_t node = (size_t)(-pq.top().second);
         pq.pop();
         newoff[node] = (int32_t)(4 * order.size());
         order.push_back(node);
         for (int ch = 0; ch < 2; ++ch) {
-            int32_t idx;
-            std::memcpy(&idx, &dm.nodes[4 * node + 3].x + ch, 4);
+            const int32_t idx = child(node, ch);
             if (idx < 0 || newoff[idx / 4] != -1) continue;
             newoff[idx / 4] = -2;                          // queued
             pq.push({ child_area(node, ch), -(int64_t)(idx / 4) });
+        }
+    }
+    // the rest: depth-first from the frontier, the two children of a node
+    // placed side by side (a ray that enters one often enters the other, and
+    // they share a cache line)
+    std::vector<size_t> frontier;
+    while (!pq.empty()) { frontier.push_back((size_t)(-pq.top().second)); pq.pop(); }
+    std::sort(frontier.begin(), frontier.end(), [&](size_t a, size_t b) { return a < b; });
+    std::vector<size_t> st;
+    auto place = [&](size_t node) { newoff[node] = (int32_t)(4 * order.size()); order.push_back(node); };
+    for (size_t f : frontier) {
+        place(f);
+        st.push_back(f);
+        while (!st.empty()) {
+            const size_t node = st.back();
+            st.pop_back();
+            size_t kids[2];
+            int nk = 0;
+            for (int ch = 0; ch < 2; ++ch) {
+                const int32_t idx = child(node, ch);
+                if (idx >= 0 && newoff[idx / 4] == -1) kids[nk++] = (size_t)(idx / 4);
+            }
+            for (int k = 0; k < nk; ++k) place(kids[k]);
+            for (int k = nk - 1; k >= 0; --k) st.push_back(kids[k]);   // first child's subtree next
         }
     }
     std::vector<vr4> out(4 * order.size());
@@ -645,7 +679,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
         p.counters = c->counters;
     }
-#if defined(VR_TIMING) || defined(VR_LANESTATS)
+#if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS)
     if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
     p.counters = c->counters;   // diagnostic build: phase timers in slots 8..13
 #endif
