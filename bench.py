@@ -204,7 +204,7 @@ def main():
             "bytes_per_path": round(bytes_per_launch / max(own_paths, 1), 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "render_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "kernel": "render_wave_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                          "launches": launches},
         }
         if not args.no_cpu and world == 1:
