@@ -30,7 +30,8 @@ def main():
     lines += [f"| {k} | {v:.4g} |" for k, v in sorted(m.items())]
     g = m.get("GRBM_GUI_ACTIVE")
     if g:
-        lines += ["", "Derived (per CU, over GRBM_GUI_ACTIVE cycles):", ""]
+        g = g / 8.0      # GRBM_GUI_ACTIVE sums the 8 XCDs (checked against the kernel's duration)
+        lines += ["", "Derived (per CU, over the kernel's cycles = GRBM_GUI_ACTIVE / 8 XCDs):", ""]
         for k, label in (("TA_TA_BUSY_sum", "TA busy"), ("TD_TD_BUSY_sum", "TD busy"),
                          ("TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TA address stalled by TC"),
                          ("TA_DATA_STALLED_BY_TC_CYCLES_sum", "TA data stalled by TC"),
