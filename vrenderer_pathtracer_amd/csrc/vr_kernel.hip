@@ -184,6 +184,10 @@ constexpr int cache_nodes(int stack, int extra = 0) {
 // Raw buffer loads for the node and triangle arrays: a 32-bit lane offset
 // against an SGPR descriptor (bounds-checked, no 64-bit address math), and an
 // explicit width per fetch (16 B node rows, 8 B child indices, 12 B vertices).
+// cache policy bits of the triangle loads (aux operand of the buffer loads)
+#ifndef VR_TRI_CPOL
+#define VR_TRI_CPOL 0
+#endif
 typedef unsigned int vr_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int vr_u32x3 __attribute__((ext_vector_type(3)));
 typedef unsigned int vr_u32x4 __attribute__((ext_vector_type(4)));
@@ -195,7 +199,7 @@ __device__ __forceinline__ vr4 buf_load4(__amdgpu_buffer_rsrc_t b, int off) {
     return mk4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 __device__ __forceinline__ vr3 buf_load3(__amdgpu_buffer_rsrc_t b, int off) {
-    const vr_u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(b, off, 0, 0);
+    const vr_u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(b, off, 0, VR_TRI_CPOL);
     return vr3{ __uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z) };
 }
 __device__ __forceinline__ int2 buf_load2i(__amdgpu_buffer_rsrc_t b, int off) {
