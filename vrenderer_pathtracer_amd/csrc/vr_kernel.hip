@@ -202,6 +202,10 @@ __device__ __forceinline__ vr3 buf_load3(__amdgpu_buffer_rsrc_t b, int off) {
     const vr_u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(b, off, 0, VR_TRI_CPOL);
     return vr3{ __uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z) };
 }
+__device__ __forceinline__ int4 buf_load4i(__amdgpu_buffer_rsrc_t b, int off) {
+    const vr_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, 0);
+    return make_int4((int)v.x, (int)v.y, (int)v.z, (int)v.w);
+}
 __device__ __forceinline__ int2 buf_load2i(__amdgpu_buffer_rsrc_t b, int off) {
     const vr_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(b, off, 0, 0);
     return make_int2((int)v.x, (int)v.y);
@@ -400,6 +404,61 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
 #endif
 }
 
+// One visit of a 4-wide node (F_WIDE, t-culled mode only): four slab tests
+// against the exact fp32 boxes of the collapsed binary tree, the entered
+// children ordered by entry distance, the nearest next and the others pushed
+// far to near.  Visits half as many nodes per ray as the binary walk; the
+// closest hit is the same (only the order among equal-distance hits can
+// differ, as for any culled order).
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
+{
+    int* stk = L.stk;
+    if (COUNT) cnt.nodes++;
+    VR_LANE(0, 1);
+    const __amdgpu_buffer_rsrc_t b4 = buf_rsrc(p.bvh4, p.n_nodes4 * 112u);
+    const int off = tr.nodeAddr * 16;
+    const vr4 lx = buf_load4(b4, off), hx = buf_load4(b4, off + 16);
+    const vr4 ly = buf_load4(b4, off + 32), hy = buf_load4(b4, off + 48);
+    const vr4 lz = buf_load4(b4, off + 64), hz = buf_load4(b4, off + 80);
+    const int4 ci = buf_load4i(b4, off + 96);
+    auto sl = [&](float n, float iv, float od) { return __builtin_fmaf(n, iv, -od); };
+    float key[4];
+    int val[4];
+    auto child = [&](int i, float lxi, float hxi, float lyi, float hyi, float lzi, float hzi, int idx) {
+        const float a0 = sl(lxi, tr.ivx, tr.odx), a1 = sl(hxi, tr.ivx, tr.odx);
+        const float b0 = sl(lyi, tr.ivy, tr.ody), b1 = sl(hyi, tr.ivy, tr.ody);
+        const float c0 = sl(lzi, tr.ivz, tr.odz), c1 = sl(hzi, tr.ivz, tr.odz);
+        const float tmin = span_begin(a0, a1, b0, b1, c0, c1, 0.0f);
+        const float tmax = span_end(a0, a1, b0, b1, c0, c1, 1e20f);
+        const bool hit = (tmax >= tmin) && (tmin <= tr.tcull) && (idx != kSentinel);
+        key[i] = hit ? tmin : __builtin_inff();
+        val[i] = idx;
+    };
+    child(0, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, ci.x);
+    child(1, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, ci.y);
+    child(2, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, ci.z);
+    child(3, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, ci.w);
+    const int n = (key[0] != __builtin_inff()) + (key[1] != __builtin_inff()) + (key[2] != __builtin_inff()) +
+                  (key[3] != __builtin_inff());
+    auto cs = [&](int i, int j) {                          // compare-swap, ties keep slot order
+        const bool sw = key[j] < key[i];
+        const float ki = key[i], kj = key[j];
+        const int vi = val[i], vj = val[j];
+        key[i] = sw ? kj : ki; key[j] = sw ? ki : kj;
+        val[i] = sw ? vj : vi; val[j] = sw ? vi : vj;
+    };
+    cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+    const int top = stk[tr.sp * kBlockThreads];
+    if (n >= 4) stk[(tr.sp + 1) * kBlockThreads] = val[3];
+    tr.sp += n >= 4 ? 1 : 0;
+    if (n >= 3) stk[(tr.sp + 1) * kBlockThreads] = val[2];
+    tr.sp += n >= 3 ? 1 : 0;
+    if (n >= 2) stk[(tr.sp + 1) * kBlockThreads] = val[1];
+    tr.sp += n >= 2 ? 1 : (n == 0 ? -1 : 0);
+    tr.nodeAddr = n == 0 ? top : val[0];
+}
+
 // intersectTriangle (RayIntersection.cuh:54-111) for compact triangle k and
 // the closest-hit update (:379-386).  Evaluated branch-free: every early
 // return of the reference becomes a term of the final predicate (the values
@@ -451,7 +510,8 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
     int* stk = L.stk;
     int leafAddr = 0;
     while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
-        node_step<COUNT, FEAT>(p, r, tr, L, cnt);
+        if (HAS(F_WIDE)) node_step4<COUNT, FEAT>(p, r, tr, L, cnt);
+        else node_step<COUNT, FEAT>(p, r, tr, L, cnt);
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
             leafAddr = tr.nodeAddr;
             tr.nodeAddr = trav_pop(tr, stk);
@@ -930,7 +990,7 @@ __device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, 
     L.idx = lds_idx;
     L.n_cached = 0;
 #ifndef VR_NO_NODE_CACHE
-    if (HAS(F_MESH)) {
+    if (HAS(F_MESH) && !HAS(F_WIDE)) {
         if (kFp16Nodes && !HAS(F_STRICT)) {            // fp16 nodes, 32 B: 1.5x as many fit
             const uint32_t cap = (uint32_t)(3 * cn / 2);
             L.n_cached = (int)(p.n_nodes < cap ? p.n_nodes : cap);
@@ -1535,11 +1595,11 @@ __global__ void selftest_math_kernel(int fn, const float* a, const float* b, flo
 // Feature specialisations, smallest first (BASELINE configs C1..C5); the
 // generic kernel covers everything else, deep trees and the counting variant.
 constexpr uint32_t kFeatAll =
-    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT;
-constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH;                                   // C2, Cornell-only
+    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT | F_WIDE;
+constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH | F_WIDE;                          // C2, Cornell-only
 constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                              // C1
-constexpr uint32_t kFeatHdriMesh = F_MESH;                                                  // C5
-constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;        // C3
+constexpr uint32_t kFeatHdriMesh = F_MESH | F_WIDE;                                         // C5
+constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_WIDE; // C3
 constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
 
 template <uint32_t FEAT>

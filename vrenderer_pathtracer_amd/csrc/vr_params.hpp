@@ -22,6 +22,7 @@ enum Flags : uint32_t {
     F_TEX_NORM = 1u << 6,    // kHasNormalMap       (:26)
     F_TEX_SPEC = 1u << 7,    // kHasSpecularMap     (:27)
     F_STRICT = 1u << 8,      // visit every pierced box, as the reference (no t-culling)
+    F_WIDE = 1u << 9,        // culled traversal over the 4-wide collapse of the tree (bvh4)
 };
 
 constexpr int kMaxFramesPerLaunch = 64;
@@ -44,6 +45,8 @@ struct RenderParams {
     uint32_t path_stride;            // owned tiles * 256 (scratch row length)
     vr4* paths;                      // per-path results [2*n_frames][path_stride]
     const vr4* bvh;
+    const vr4* bvh4;                 // 4-wide nodes, 7 rows each (culled traversal, VR_BVH4)
+    uint32_t n_nodes4;
     const vr4* bvh16;                // same nodes, conservative fp16 boxes, 32 B each (culled traversal)
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
     const vr3* verts;                // 3 vertices per triangle, compact leaf order

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <array>
 #include <queue>
 #include <string>
 #include <unordered_map>
@@ -61,9 +62,9 @@ struct vrhip_ctx {
     bool cornell = false, example = false, view_brdf = false;
     bool strict = false;          // exact reference traversal (no t-culling)
     // mesh
-    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr3* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
+    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr4* bvh4 = nullptr; vr3* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
-    uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0;
+    uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0, dev_nodes4 = 0;
     bool mesh = false;
     // environment / textures / brdf
     vr4* hdr = nullptr; uint32_t hdr_w = 0, hdr_h = 0;
@@ -126,6 +127,7 @@ uint32_t owned_tiles_of(uint32_t W, uint32_t H, uint32_t rank, uint32_t n_ranks)
 struct DeviceMesh {
     std::vector<vr4> nodes, normals, tangents;
     std::vector<vr4> nodes16;        // 2 x 16 B per node: conservative fp16 boxes + child indices
+    std::vector<vr4> nodes4;         // 4-wide nodes, 7 x 16 B each (collapsed binary tree)
     std::vector<vr3> tris;           // packed 12 B vertices (vertex .w never reaches a result)
     std::vector<vr2> uvs;
 };
@@ -272,6 +274,72 @@ void build_nodes16(DeviceMesh& dm)
     }
 }
 
+// 4-wide collapse of the binary tree for the t-culled traversal: a 4-node
+// holds the grandchildren of a binary node (a child that is a leaf is kept
+// as is), with the exact fp32 boxes the binary parents store.  Layout per
+// node (7 rows): lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] child[4];
+// child >= 0: 4-node index * 7 (row offset); < 0: leaf code; empty slots
+// hold the sentinel 0x76543210 and are masked out by the traversal.
+void build_nodes4(DeviceMesh& dm)
+{
+    const size_t n = dm.nodes.size() / 4;
+    dm.nodes4.clear();
+    if (n == 0) return;
+    struct Child { float lo[3], hi[3]; int32_t idx; };
+    auto bin_child = [&](size_t node, int ch) {
+        Child c;
+        const vr4 a = dm.nodes[4 * node + ch], z = dm.nodes[4 * node + 2], ni = dm.nodes[4 * node + 3];
+        c.lo[0] = a.x; c.hi[0] = a.y; c.lo[1] = a.z; c.hi[1] = a.w;
+        c.lo[2] = ch ? z.z : z.x; c.hi[2] = ch ? z.w : z.y;
+        std::memcpy(&c.idx, ch ? &ni.y : &ni.x, 4);
+        return c;
+    };
+    std::vector<int32_t> id4(n, -1);          // binary node -> 4-node index
+    std::vector<size_t> queue{ 0 };
+    id4[0] = 0;
+    std::vector<std::array<Child, 4>> kids;
+    std::vector<int> nkids;
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const size_t b = queue[qi];
+        std::array<Child, 4> k4;
+        int nk = 0;
+        for (int ch = 0; ch < 2; ++ch) {
+            const Child c = bin_child(b, ch);
+            if (c.idx >= 0) {                 // inner: take its two children
+                const size_t cb = (size_t)c.idx / 4;
+                k4[nk++] = bin_child(cb, 0);
+                k4[nk++] = bin_child(cb, 1);
+            } else {
+                k4[nk++] = c;
+            }
+        }
+        for (int k = 0; k < nk; ++k) {
+            if (k4[k].idx >= 0) {
+                const size_t cb = (size_t)k4[k].idx / 4;
+                if (id4[cb] < 0) { id4[cb] = (int32_t)queue.size(); queue.push_back(cb); }
+            }
+        }
+        kids.push_back(k4);
+        nkids.push_back(nk);
+    }
+    dm.nodes4.assign(7 * queue.size(), vr4{ 0, 0, 0, 0 });
+    for (size_t i = 0; i < queue.size(); ++i) {
+        float* r = &dm.nodes4[7 * i].x;     // 28 floats
+        for (int k = 0; k < 4; ++k) {
+            if (k < nkids[i]) {
+                const Child& c = kids[i][k];
+                for (int a = 0; a < 3; ++a) { r[8 * a + k] = c.lo[a]; r[8 * a + 4 + k] = c.hi[a]; }
+                const int32_t idx = c.idx >= 0 ? 7 * id4[(size_t)c.idx / 4] : c.idx;
+                std::memcpy(&r[24 + k], &idx, 4);
+            } else {
+                for (int a = 0; a < 3; ++a) { r[8 * a + k] = 0.f; r[8 * a + 4 + k] = 0.f; }
+                const int32_t empty = 0x76543210;  // the traversal's sentinel: never entered
+                std::memcpy(&r[24 + k], &empty, 4);
+            }
+        }
+    }
+}
+
 bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const vr4* normals,
                       const vr4* tangents, const vr2* uvs, DeviceMesh& dm, std::string& why)
 {
@@ -321,6 +389,7 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
     order_nodes_by_area(dm);
 #endif
     build_nodes16(dm);
+    build_nodes4(dm);
     if (dm.tris.empty()) {
         dm.tris.push_back(vr3{ 0, 0, 0 });
         dm.normals.push_back(vr4{ 0, 0, 0, 0 });
@@ -398,7 +467,7 @@ int vrhip_destroy(vrhip_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->accum); dfree(c->rgba); dfree(c->depth);
-    dfree(c->bvh); dfree(c->bvh16); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
+    dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     for (int i = 0; i < 2; ++i)
         if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
@@ -467,6 +536,8 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     const size_t nt = dm.tris.size();
     if ((rc = upload(c, c->bvh, dm.nodes.data(), dm.nodes.size() * 16))) return rc;
     if ((rc = upload(c, c->bvh16, dm.nodes16.data(), dm.nodes16.size() * 16))) return rc;
+    if ((rc = upload(c, c->bvh4, dm.nodes4.data(), dm.nodes4.size() * 16))) return rc;
+    c->dev_nodes4 = (uint32_t)(dm.nodes4.size() / 7);
     if ((rc = upload(c, c->verts, dm.tris.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->normals, dm.normals.data(), nt * 16))) return rc;
     if ((rc = upload(c, c->tangents, dm.tangents.data(), nt * 16))) return rc;
@@ -659,6 +730,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     if (c->example) f |= vr::F_EXAMPLE;
     if (c->view_brdf) f |= vr::F_VIEW_BRDF;
     if (c->strict) f |= vr::F_STRICT;
+#ifdef VR_BVH4
+    if (!c->strict && c->mesh && c->bvh_depth <= 30) f |= vr::F_WIDE;   // <= 3 pushes per 4-wide level
+#endif
     if (c->mesh) f |= vr::F_MESH;
     if (c->brdf) f |= vr::F_BRDF;
     if (c->tex[0]) f |= vr::F_TEX_DIFF;
@@ -667,13 +741,16 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.flags = f;
     p.tiles_x = p.wr / 16u;
     p.rank = c->rank; p.nranks = c->nranks;
+    p.bvh4 = c->bvh4; p.n_nodes4 = c->mesh ? c->dev_nodes4 : 0;
     p.bvh = c->bvh; p.bvh16 = c->bvh16; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
     p.hdr = c->hdr; p.hdr_w = c->hdr_w; p.hdr_h = c->hdr_h;
     for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
     p.brdf = c->brdf;
     p.accum = c->accum; p.rgba = c->rgba; p.depth = c->depth;
     const uint32_t n_tiles = owned_tiles_of(c->W, c->H, c->rank, c->nranks);
-    const int stack = c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 30 ? 32 : 64;   // entries needed: depth + 1
+    // stack entries needed: binary walk depth + 1; 4-wide walk 3 per 4-level + 1
+    const int stack = (f & vr::F_WIDE) ? (c->bvh_depth <= 15 ? 32 : 64)
+                                       : (c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 30 ? 32 : 64);
     if (count) {
         if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
