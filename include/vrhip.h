@@ -120,6 +120,14 @@ int vrhip_upload_brdf(vrhip_ctx *ctx, const float *table, size_t n_floats);
  * short file (the reference prints and returns nullptr). */
 int vrhip_load_merl(const char *path, float *table, size_t n_floats);
 
+/* replaces the OpenEXR read in NGLScene::loadHDRMap (src/NGLScene.cpp:205-231,
+ * Imf::RgbaInputFile over the data window): a single-part scanline .exr
+ * (NONE, RLE, ZIPS or ZIP compression; HALF/FLOAT/UINT channels) as half RGBA
+ * (Imf::Rgba layout, FLOAT samples rounded to half; missing R/G/B = 0,
+ * A = 1), ready for vrhip_upload_hdr_half.  Pass rgba_half = NULL to query
+ * the size.  Host only. */
+int vrhip_load_exr(const char *path, uint16_t *rgba_half, size_t n_values, uint32_t *width, uint32_t *height);
+
 /* ---- display interop ---------------------------------------------------- */
 /* replaces vRendererCuda::registerTextureBuffer / registerDepthBuffer
  * (src/vRendererCuda.cpp:57-67): registers an OpenGL texture (which = 0:

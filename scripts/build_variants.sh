@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p variants
-SRC="vrenderer_pathtracer_amd/csrc/vr_kernel.hip vrenderer_pathtracer_amd/csrc/vrhip_api.cpp vrenderer_pathtracer_amd/csrc/vr_bvh.cpp"
+SRC="vrenderer_pathtracer_amd/csrc/vr_kernel.hip vrenderer_pathtracer_amd/csrc/vrhip_api.cpp vrenderer_pathtracer_amd/csrc/vr_bvh.cpp vrenderer_pathtracer_amd/csrc/vr_exr.cpp -lz"
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
   ( rm -f variants/libvrhip_$name.so

@@ -221,3 +221,45 @@ def test_load_merl_matches_reference_layout(native, tmp_path):
         fh.write(vals[:1000].astype(np.float64).tobytes())
     with pytest.raises(_native.VRHIPError):
         load_merl(short)
+
+
+@pytest.mark.parametrize("compression,ptype,channels,origin", [
+    (0, 1, "RGBA", (0, 0)), (3, 2, "RGB", (0, 0)), (2, 1, "RGBA", (3, 5)), (1, 1, "RGBA", (0, 0)),
+    (3, 1, "BGR", (-2, 7)), (1, 2, "A", (0, 0))])
+def test_load_exr_roundtrip(native, tmp_path, compression, ptype, channels, origin):
+    """vrhip_load_exr (vr_exr.cpp) against tests/exr_writer.py: half RGBA over the
+    data window, FLOAT samples rounded to half, missing R/G/B = 0 and A = 1."""
+    from exr_writer import write_exr
+    from vrenderer_pathtracer_amd.renderer import load_exr
+    rng = np.random.default_rng(compression * 10 + ptype)
+    h, w = 37, 53
+    img = (rng.random((h, w, 4)) * 8.0).astype(np.float32)
+    img[5:20, 10:30] = 2.5                                   # flat region: RLE runs
+    f = tmp_path / "t.exr"
+    write_exr(f, img, channels=channels, pixel_type=ptype, compression=compression, origin=origin)
+    got = load_exr(f)
+    assert got.shape == (h, w, 4) and got.dtype == np.float16
+    exp = np.zeros((h, w, 4), np.float16)
+    exp[..., 3] = 1.0
+    for c in channels:
+        exp[..., "RGBA".index(c)] = img[..., "RGBA".index(c)].astype(np.float16)
+    assert np.array_equal(got.view(np.uint16), exp.view(np.uint16))
+
+
+def test_load_exr_rejects_unsupported(native, tmp_path):
+    from exr_writer import write_exr
+    from vrenderer_pathtracer_amd.renderer import load_exr
+    img = np.ones((8, 8, 4), np.float32)
+    f = tmp_path / "piz.exr"
+    write_exr(f, img, compression=0)
+    data = bytearray(open(f, "rb").read())
+    i = data.find(b"compression\0compression\0") + len(b"compression\0compression\0") + 4
+    data[i] = 4                                              # PIZ
+    open(f, "wb").write(bytes(data))
+    with pytest.raises(_native.VRHIPError):
+        load_exr(f)
+    with pytest.raises(_native.VRHIPError):
+        load_exr(tmp_path / "missing.exr")
+    (tmp_path / "junk.exr").write_bytes(b"not an exr file at all")
+    with pytest.raises(_native.VRHIPError):
+        load_exr(tmp_path / "junk.exr")

@@ -6,7 +6,7 @@ reference's vRenderer interface (renderer.VRendererHIP), the procedural
 scenes used by the benchmark and tests, and the build script.
 """
 from .build import build as build_native, LIB_PATH  # noqa: F401
-from .renderer import (VRendererHIP, Camera, build_flat, validate_flat, selftest_math, load_merl,  # noqa: F401
+from .renderer import (VRendererHIP, Camera, build_flat, validate_flat, selftest_math, load_merl, load_exr,  # noqa: F401
                        device_count, DIFFUSE, NORMAL, SPECULAR)
 from ._native import VRHIPError  # noqa: F401
 

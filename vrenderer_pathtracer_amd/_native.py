@@ -53,6 +53,7 @@ _SIGNATURES = {
     "vrhip_upload_texture": (ctypes.c_int, [_ctx, ctypes.c_int, _f, ctypes.c_uint32, ctypes.c_uint32]),
     "vrhip_upload_brdf": (ctypes.c_int, [_ctx, _f, ctypes.c_size_t]),
     "vrhip_load_merl": (ctypes.c_int, [ctypes.c_char_p, _f, ctypes.c_size_t]),
+    "vrhip_load_exr": (ctypes.c_int, [ctypes.c_char_p, _u16, ctypes.c_size_t, _u32, _u32]),
     "vrhip_gl_register_image": (ctypes.c_int, [_ctx, ctypes.c_int, ctypes.c_uint, ctypes.c_uint]),
     "vrhip_gl_present": (ctypes.c_int, [_ctx]),
     "vrhip_render": (ctypes.c_int, [_ctx, ctypes.c_uint32, _u32, ctypes.c_uint32]),

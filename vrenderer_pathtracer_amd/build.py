@@ -14,8 +14,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libvrhip.so")
-SOURCES = ["vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp"]
-HEADERS = ["vr_params.hpp", "vr_math.hpp", "vr_bvh.hpp"]
+SOURCES = ["vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp", "vr_exr.cpp"]
+HEADERS = ["vr_params.hpp", "vr_math.hpp", "vr_bvh.hpp", "vr_exr.hpp"]
 ARCH = os.environ.get("VRHIP_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: results are defined without FMA contraction (parity
@@ -47,7 +47,7 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None) -> str:
         return LIB_PATH
     tmp = LIB_PATH + ".tmp"
     cmd = [_hipcc()] + HIPCC_FLAGS + list(extra_flags or []) + ["-o", tmp] + \
-          [os.path.join(CSRC, s) for s in SOURCES]
+          [os.path.join(CSRC, s) for s in SOURCES] + ["-lz"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     res = subprocess.run(cmd, capture_output=True, text=True)

@@ -21,6 +21,7 @@
 
 #include "../../include/vrhip.h"
 #include "vr_bvh.hpp"
+#include "vr_exr.hpp"
 #include "vr_params.hpp"
 
 using vr::vr3;
@@ -625,6 +626,21 @@ int vrhip_load_merl(const char* path, float* table, size_t n_floats)
     f.read(reinterpret_cast<char*>(d.data()), (std::streamsize)(3 * n * sizeof(double)));
     if (!f) return fail(VRHIP_ERR_INVALID, "truncated MERL file");
     for (size_t i = 0; i < 3 * n; ++i) table[i] = (float)d[i];
+    return VRHIP_OK;
+}
+
+int vrhip_load_exr(const char* path, uint16_t* rgba_half, size_t n_values, uint32_t* width, uint32_t* height)
+{
+    if (!path || !width || !height) return fail(VRHIP_ERR_INVALID, "null argument");
+    std::vector<uint16_t> px;
+    uint32_t w = 0, h = 0;
+    std::string why;
+    if (vr::read_exr_rgba_half(path, px, w, h, why) != 0) return fail(VRHIP_ERR_INVALID, why);
+    *width = w;
+    *height = h;
+    if (!rgba_half) return VRHIP_OK;                 // size query
+    if (n_values < px.size()) return fail(VRHIP_ERR_INVALID, "output too small for 4*w*h half values");
+    std::memcpy(rgba_half, px.data(), px.size() * 2);
     return VRHIP_OK;
 }
 

@@ -89,6 +89,21 @@ def load_merl(path: str) -> np.ndarray:
     return out
 
 
+def load_exr(path: str) -> np.ndarray:
+    """The HDRI read of NGLScene::loadHDRMap (src/NGLScene.cpp:205-231,
+    Imf::RgbaInputFile) through the C ABI: float16 (H, W, 4) RGBA over the data
+    window, ready for VRendererHIP.loadHDR."""
+    L = _native.lib()
+    w = ctypes.c_uint32(0)
+    h = ctypes.c_uint32(0)
+    p = str(path).encode()
+    check(L.vrhip_load_exr(p, None, 0, ctypes.byref(w), ctypes.byref(h)), "vrhip_load_exr")
+    out = np.zeros((h.value, w.value, 4), np.uint16)
+    check(L.vrhip_load_exr(p, out.ctypes.data_as(_native._u16), out.size, ctypes.byref(w), ctypes.byref(h)),
+          "vrhip_load_exr")
+    return out.view(np.float16)
+
+
 class Camera:
     """Host camera state, the reference's Camera (src/Camera.cpp) reduced to
     what the renderer consumes: origin, dir, up, right, fovScale."""
