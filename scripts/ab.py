@@ -3,7 +3,7 @@
 
   python scripts/ab.py [--cfg C2] [--frames 8] [--steps 4] lib1.so lib2.so ...
 
-Prints Mpaths/s per variant (median of steps) and checks every variant's
+Prints Mpaths/s per variant (median of 3 batches of back-to-back steps) and checks every variant's
 accumulation buffer bit-equals the first one's.
 """
 import argparse
@@ -27,10 +27,13 @@ F = {frames}
 r.render(frames=F, time_seed=sc["time"])     # warm-up
 r.clearBuffer()
 ts = []
-for i in range({steps}):
+for b in range(3):     # batches of back-to-back steps (as bench.py issues them), synced at the end
     t0 = time.perf_counter()
-    r.render(frames=F, times=[sc["time"] + i * F + k for k in range(F)])
-    ts.append(time.perf_counter() - t0)
+    for i in range({steps}):
+        j = b * {steps} + i
+        r.render(frames=F, times=[sc["time"] + j * F + k for k in range(F)], sync=False)
+    r.sync()
+    ts.append((time.perf_counter() - t0) / {steps})
 acc = r.read_accum()
 wr, hr = (sc["width"] // 16) * 16, (sc["height"] // 16) * 16
 paths = wr * hr * 2 * F

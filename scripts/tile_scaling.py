@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Projected strong scaling of the band sharding, measured on ONE GPU.
 
-  python scripts/tile_scaling.py [C2] [frames_per_step] [path_split, 0 = auto]
+  python scripts/tile_scaling.py [C2] [frames_per_step] [path_split, 0 = auto] [N list, e.g. 1,8]
 
 For N in 1, 2, 4, 8 this renders rank 0's share of an N-way band split (rank
 0 owns the most tiles) and reports the kernel time per step, the projected
@@ -22,6 +22,7 @@ from vrenderer_pathtracer_amd import VRendererHIP, scenes  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
 F = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 SPLIT = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+NS = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
 sc = scenes.make_scene(cfg)
 W, H = sc["width"], sc["height"]
 paths = (W // 16) * 16 * (H // 16) * 16 * 2 * F
@@ -29,7 +30,7 @@ r = VRendererHIP(0)
 scenes.load_into(r, sc)
 r.set_path_split(SPLIT)
 base = None
-for n in (1, 2, 4, 8):
+for n in NS:
     r.set_tiling(0, n)
     r.clearBuffer()
     for i in range(2):

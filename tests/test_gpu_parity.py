@@ -221,6 +221,55 @@ def test_multi_frame_launch_equals_frame_by_frame(native):
     assert np.array_equal(a4.view(np.uint32), a1.view(np.uint32))
 
 
+def test_pipelined_steps_bitexact_vs_portable_oracle(native, oracle):
+    """Back-to-back render calls without a sync (the launches of consecutive
+    calls overlap on the two path streams) accumulate exactly what the
+    oracle's frame-by-frame loop does."""
+    sc = scenes.make_scene("C2", 96, 64)
+    times = [sc["time"] + 3 * i for i in range(7)]
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.render(frames=2, times=times[0:2], sync=False)
+    r.render(frames=1, times=times[2:3], sync=False)
+    r.render(frames=4, times=times[3:7], sync=False)
+    got = r.read_accum(), r.read_rgba8(), r.read_depth8()
+    assert r.getFrameCount() == 7
+    r.cleanUp()
+    ref = po.render(sc, frames=7, times=times, libm=po.LIBM_PORTABLE)
+    for g, o, what in zip(got, ref, ("accum", "rgba8", "depth8")):
+        assert_bitexact(g, o, sc, what)
+
+
+@pytest.mark.parametrize("cfg", ["C3", "C4"])
+def test_pipelined_steps_with_scene_changes_equal_synchronous(native, cfg):
+    """Uploads, Fresnel and tiling changes between unsynchronised render calls
+    take effect exactly where they were issued (the path streams join the
+    render stream after any buffer change)."""
+    sc = scenes.make_scene(cfg, 96, 64)
+    t = sc["time"]
+
+    def run(sync):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.render(frames=2, times=[t, t + 1], sync=sync)
+        r.render(frames=3, times=[t + 2, t + 3, t + 4], sync=sync)
+        r.loadHDR(np.ascontiguousarray(sc["hdr"][::-1]))
+        r.render(frames=2, times=[t + 5, t + 6], sync=sync)
+        r.setFresnelCoef(0.4)
+        r.render(frames=1, times=[t + 7], sync=sync)
+        r.set_tiling(0, 2)
+        r.render(frames=2, times=[t + 8, t + 9], sync=sync)
+        out = r.read_accum(), r.read_rgba8(), r.getFrameCount()
+        r.cleanUp()
+        return out
+
+    a_sync, c_sync, n_sync = run(True)
+    a_pipe, c_pipe, n_pipe = run(False)
+    assert n_sync == n_pipe
+    assert np.array_equal(a_sync.view(np.uint32), a_pipe.view(np.uint32))
+    assert np.array_equal(c_sync, c_pipe)
+
+
 @pytest.mark.parametrize("cfg,w,h", [("C2", 96, 64), ("C3", 96, 64), ("C4", 96, 64)])
 def test_strict_counts_equal_oracle_counts(native, oracle, cfg, w, h):
     """Strict traversal visits exactly the nodes and tests exactly the

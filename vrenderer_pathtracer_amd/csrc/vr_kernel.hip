@@ -955,6 +955,8 @@ __device__ __forceinline__ u8x4 tonemap(vr4 io, uint32_t frame) {
 __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParams p)
 {
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
+    // the path kernel's queue heads, for the next launch on this scratch
+    if (tile == 0 && tid < VR_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride] = 0u;
     const int wave = (int)tid >> 6, lane = (int)tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
     const uint32_t tile_y = gtile / p.tiles_x;
@@ -1114,19 +1116,56 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     }
 }
 
-// Path-pool variant of render (the default): each wave owns the paths
-// [q0, q1) of its 8x8 sub-tile's 64 pixels as a pool of 64*(q1-q0) items
-// (item i: pixel i % 64, path q0 + i / 64).  A lane runs one path at a time;
-// when its path ends it stores the path's radiance to p.paths and takes the
-// next item of the pool, so lanes whose rays finish early do not idle while
-// the wave's other lanes traverse.  Traversal is paused between outer
-// iterations (trav_iter) once VR_SHADE_BATCH lanes wait for shading.  Every
-// path runs exactly the operations of trace(); only the interleaving of
-// different paths on the SIMD changes, so results are bit-identical.
+// Primary hits, one thread per owned pixel: the camera ray's closest hit
+// (the HitRec intersect_scene returns: t, kind, idx, barycentrics,
+// example-sphere u,v), two float4s per pixel in the scratch order of
+// p.paths, read by every path of the pixel in render_wave_kernel.  One ray
+// per thread, so no LDS node cache.
+template <int STACK, uint32_t FEAT>
+__global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderParams p)
+{
+    __shared__ int lds_stack[STACK * kBlockThreads];
+    const int tid = threadIdx.x;
+    Lds L;
+    L.stk = lds_stack + tid;
+    L.nodes = nullptr;
+    L.idx = nullptr;
+    L.n_cached = 0;
+    const uint32_t tile = blockIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
+    const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
+    Cnt cnt;
+    HitRec hr;
+    (void)intersect_scene<STACK, false, FEAT>(p, camera_ray(p, x, y), hr, L, cnt);
+    vr4* dst = p.prim + 2u * ((size_t)tile * kBlockThreads + tid);
+    dst[0] = mk4(hr.t, __int_as_float(hr.kind), __int_as_float(hr.idx), hr.bu);
+    dst[1] = mk4(hr.bv, hr.su, hr.sv, 0.f);
+}
+
+// Path-pool render (the default for mesh scenes), a persistent kernel over
+// work queues.  The launch's paths are cut into chunks of 64 items: chunk =
+// (sub-tile s, path q), s an 8x8 quadrant of one of the rank's tiles, item i
+// = pixel i of s.  The grid is one resident wave set; each wave takes chunks
+// from the queues and its lanes run one path each through a small state
+// machine (setup = sphere tests, traverse the mesh, shade).  A lane whose path
+// ends stores the radiance to p.paths[q][pixel] and takes the next item
+// (ballot + mbcnt give each idle lane its item in one wave-uniform step), so
+// lanes whose rays finish early do not idle while the wave's other lanes
+// traverse, and no wave waits at the end of the launch for blocks of uneven
+// cost.  Traversal pauses between outer iterations (trav_iter) once
+// VR_SHADE_BATCH lanes wait for shading.
+//
+// Primary hits: the camera ray is the same for every path of a pixel (no
+// jitter, PathTracer.cu:842-844), so primary_kernel traces it once per pixel
+// per launch and every path of the pixel starts at its shading.
+//
+// Every path runs exactly the operations of trace(); only the interleaving
+// of paths on the SIMD changes, so results are bit-identical.
 // finish_kernel then sums each pixel's paths in path order.
-// Traversal pauses for shading once VR_SHADE_BATCH lanes wait for it and
-// they are at least 1/VR_SHADE_RATIO of the lanes still traversing
-// (measured on C2/C3: 16 and 1; the choice moves results by < 1 %).
 #ifndef VR_SHADE_BATCH
 #define VR_SHADE_BATCH 16
 #endif
@@ -1144,41 +1183,69 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
     __shared__ int2 lds_idx[CN];
     const int tid = threadIdx.x;
     const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
-    const uint32_t T = p.split;
-    const uint32_t tile = blockIdx.x / T;
-    const uint32_t g = blockIdx.x - tile * T;
-    const int wave = tid >> 6, lane = tid & 63;
-    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
-    const uint32_t tile_y = gtile / p.tiles_x;
-    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
-    const uint32_t x0 = tile_x * 16u + (uint32_t)((wave & 1) * 8);
-    const uint32_t y0 = tile_y * 16u + (uint32_t)((wave >> 1) * 8);
+    const int lane = tid & 63;
     const uint32_t n_paths = 2u * p.n_frames;
-    const uint32_t chunk = (n_paths + T - 1u) / T;
-    const uint32_t q0 = g * chunk < n_paths ? g * chunk : n_paths;
-    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
-    const uint32_t pool = 64u * (q1 - q0);
-    vr4* const out_base = p.paths + (size_t)tile * kBlockThreads + (size_t)wave * 64u;
+    const uint32_t n_sub = p.path_stride >> 6;             // 8x8 sub-tiles of the rank's tiles
     Cnt cnt;
 
-    uint32_t item = (uint32_t)lane;
-    uint32_t next = 64u;                                   // wave-uniform: first unassigned item
+    // Work queues: chunk c = (sub-tile c / n_paths, path c % n_paths), so the
+    // paths of one sub-tile are handed out together (coherent rays, the
+    // sub-tile's primary records in cache).  VR_QUEUES heads, queue j hands
+    // out chunks j, j + Q, j + 2Q, ... (one device-scope atomic per chunk; a
+    // single head saturates: MI355X_MICROARCH "dequeue").  A wave draws from
+    // its block's queue and, once that is drained, from the following ones.
+    constexpr uint32_t Q = VR_QUEUES;
+    const uint32_t n_chunks = n_sub * n_paths;
+    uint32_t qj = blockIdx.x % Q, drained = 0;
+    auto grab = [&](uint32_t& sub, uint32_t& path) {       // wave-uniform; sub = ~0u when no work is left
+        for (;;) {
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(p.chunk_ctr + qj * kQueueStride, 1u);
+            const uint32_t c = __builtin_amdgcn_readfirstlane(v) * Q + qj;
+            if (c < n_chunks) {
+                sub = c / n_paths;
+                path = c - sub * n_paths;
+                return;
+            }
+            if (++drained == Q) { sub = ~0u; path = 0; return; }
+            qj = qj + 1u == Q ? 0u : qj + 1u;
+        }
+    };
+#ifdef VR_WAVE_TIMES
+    const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t wpaths = 0;
+#endif
+    uint32_t cur_sub, cur_q;
+    grab(cur_sub, cur_q);                                  // wave-uniform: chunk being handed out
+    uint32_t next = 64u;                                   // items of the current chunk handed out
     int state = LS_DONE;
+    uint32_t q = 0, slot = 0;                              // this lane's path and pixel slot
     Ray ray;
     PathState ps;
     HitRec hr;
     Trav tr;
-    auto start = [&]() {                                   // render's per-sample prologue (:817-844)
-        const uint32_t px = item & 63u, q = q0 + (item >> 6), f = q >> 1;
-        const uint32_t x = x0 + (px & 7u), y = y0 + (px >> 3);
+    auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
+        if (sub == ~0u) { state = LS_DONE; return; }
+        q = path;
+        slot = sub * 64u + px;
+        const uint32_t f = q >> 1;
+        const uint32_t tile = sub >> 2, quad = sub & 3u;
+        const uint32_t gtile = p.rank + tile * p.nranks;   // tiles dealt round-robin to ranks
+        const uint32_t tile_y = gtile / p.tiles_x;
+        const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+        const uint32_t x = tile_x * 16u + (quad & 1u) * 8u + (px & 7u);
+        const uint32_t y = tile_y * 16u + (quad >> 1) * 8u + (px >> 3);
         uint32_t s1 = x * (p.first_frame + f);
         uint32_t s2 = y * p.times[f];
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
         path_begin(ps, s1, s2);
         ray = camera_ray(p, x, y);
-        state = LS_SETUP;
+        const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
+        hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
+        hr.bv = b.x; hr.su = b.y; hr.sv = b.z;
+        state = LS_SHADE;
     };
-    if (item < pool) start();
+    start(cur_sub, cur_q, (uint32_t)lane);
 
     VR_T0(t_kernel);
     for (;;) {
@@ -1199,6 +1266,11 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
                 if (n_trav == 0) break;
                 const int n_shade = __popcll(__ballot(state == LS_SHADE));
                 if (n_shade >= VR_SHADE_BATCH && n_shade * VR_SHADE_RATIO >= n_trav) break;
+#ifndef VR_NO_DRAIN_EAGER
+                // queue drained: no lane will be refilled, so a path waiting to
+                // be shaded is only delayed by the others' traversal
+                if (cur_sub == ~0u && n_shade > 0) break;
+#endif
                 if (state == LS_TRAV) {
 #ifdef VR_IFIF
                     trav_step<false, FEAT>(p, ray, tr, L, cnt);
@@ -1220,7 +1292,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
             VR_LANE(4, 5);
             vr4 out;
             if (bounce_step<false, FEAT>(p, ray, hr, ps, out, cnt)) {
-                out_base[(size_t)(q0 + (item >> 6)) * p.path_stride + (item & 63u)] = out;
+                p.paths[(size_t)q * p.path_stride + slot] = out;
                 ended = true;
             } else {
                 state = LS_SETUP;
@@ -1229,16 +1301,29 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
         VR_T1(t_shblk, 4);
         const unsigned long long em = __ballot(ended);
         if (em != 0ull) {
+            const uint32_t need = (uint32_t)__popcll(em);
+#ifdef VR_WAVE_TIMES
+            wpaths += need;
+#endif
+            uint32_t nsub = cur_sub, nq = cur_q;
+            if (next + need > 64u && cur_sub != ~0u) grab(nsub, nq);
             if (ended) {
-                item = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-                if (item < pool) start();
-                else state = LS_DONE;
+                const uint32_t r = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                if (r < 64u) start(cur_sub, cur_q, r);
+                else start(nsub, nq, r - 64u);
             }
-            next += (uint32_t)__popcll(em);
+            if (next + need > 64u) { cur_sub = nsub; cur_q = nq; next = next + need - 64u; }
+            else next += need;
         }
         if (__ballot(state != LS_DONE) == 0ull) break;
     }
+#ifdef VR_WAVE_TIMES
+    if (p.counters && lane == 0) {   // diagnostic: per-wave start / end (100 MHz) and paths completed
+        unsigned long long* w = p.counters + 16 + 3 * (blockIdx.x * 4u + (uint32_t)(tid >> 6));
+        w[0] = wt0; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = wpaths;
+    }
+#endif
     VR_T1(t_kernel, 5);
 #if defined(VR_LANESTATS) || defined(VR_TIMING) || defined(VR_NODE_STAMPS)
     if (p.counters) {
@@ -1602,8 +1687,15 @@ constexpr uint32_t kFeatHdriMesh = F_MESH | F_WIDE;                             
 constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_WIDE; // C3
 constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
 
+template <int STACK, uint32_t FEAT>
+static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
+{
+    hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT>), dim3(p.wave_blocks), dim3(kBlockThreads), 0, s, p);
+}
+
 template <uint32_t FEAT>
-static void launch_spec(const RenderParams& p, uint32_t blocks, int stack_depth, hipStream_t s)
+static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
 {
 #ifndef VR_MIN_SPEC_STACK
 #define VR_MIN_SPEC_STACK 16
@@ -1615,6 +1707,7 @@ static void launch_spec(const RenderParams& p, uint32_t blocks, int stack_depth,
 #else
     const bool wave = (FEAT & F_MESH) != 0 && (p.flags & F_MESH) != 0;
 #endif
+    const uint32_t blocks = n_tiles * p.split;
     if (!wave)
         hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
 #if defined(VR_TWO_PATHS)
@@ -1629,9 +1722,9 @@ static void launch_spec(const RenderParams& p, uint32_t blocks, int stack_depth,
         hipLaunchKernelGGL((render_block_kernel<32, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
 #else
     else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
-        hipLaunchKernelGGL((render_wave_kernel<16, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+        launch_wave<16, FEAT>(p, n_tiles, s);
     else
-        hipLaunchKernelGGL((render_wave_kernel<32, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+        launch_wave<32, FEAT>(p, n_tiles, s);
 #endif
 }
 
@@ -1647,20 +1740,20 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool
             if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
             else hipLaunchKernelGGL((render_kernel<64, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
         } else {
-            hipLaunchKernelGGL((render_wave_kernel<64, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+            launch_wave<64, kFeatAll>(p, n_tiles, s);
         }
     } else if (covers(kFeatCornellMesh)) {
-        launch_spec<kFeatCornellMesh>(p, blocks, stack_depth, s);
+        launch_spec<kFeatCornellMesh>(p, n_tiles, stack_depth, s);
     } else if (covers(kFeatCornellSphere)) {
-        launch_spec<kFeatCornellSphere>(p, blocks, stack_depth, s);
+        launch_spec<kFeatCornellSphere>(p, n_tiles, stack_depth, s);
     } else if (covers(kFeatHdriMesh)) {
-        launch_spec<kFeatHdriMesh>(p, blocks, stack_depth, s);
+        launch_spec<kFeatHdriMesh>(p, n_tiles, stack_depth, s);
     } else if (covers(kFeatHdriMeshTex)) {
-        launch_spec<kFeatHdriMeshTex>(p, blocks, stack_depth, s);
+        launch_spec<kFeatHdriMeshTex>(p, n_tiles, stack_depth, s);
     } else if (covers(kFeatHdriBrdfSphere)) {
-        launch_spec<kFeatHdriBrdfSphere>(p, blocks, stack_depth, s);
+        launch_spec<kFeatHdriBrdfSphere>(p, n_tiles, stack_depth, s);
     } else {
-        launch_spec<kFeatAll>(p, blocks, stack_depth, s);
+        launch_spec<kFeatAll>(p, n_tiles, stack_depth, s);
     }
     return (int)hipGetLastError();
 }

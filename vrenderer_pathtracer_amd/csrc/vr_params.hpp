@@ -31,6 +31,11 @@ constexpr int kMaxFramesPerLaunch = 64;
 constexpr int kCounters = 8;
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
+// render_wave_kernel work queues: VR_QUEUES counters, kQueueStride uint32 apart
+#ifndef VR_QUEUES
+#define VR_QUEUES 16
+#endif
+constexpr uint32_t kQueueStride = 256;
 
 struct RenderParams {
     vr4 cam_o, cam_d, cx, cy;        // cx, cy precomputed exactly as PathTracer.cu:833-836
@@ -44,6 +49,9 @@ struct RenderParams {
     uint32_t use_scratch;            // 1: paths store radiance to `paths`, finish_kernel accumulates
     uint32_t path_stride;            // owned tiles * 256 (scratch row length)
     vr4* paths;                      // per-path results [2*n_frames][path_stride]
+    vr4* prim;                       // per owned pixel: the camera ray's closest hit (2 x vr4, primary_kernel)
+    uint32_t* chunk_ctr;             // render_wave_kernel's work queue heads (zeroed by finish_kernel)
+    uint32_t wave_blocks;            // render_wave_kernel grid (resident blocks; the queues balance the work)
     const vr4* bvh;
     const vr4* bvh4;                 // 4-wide nodes, 7 rows each (culled traversal, VR_BVH4)
     uint32_t n_nodes4;

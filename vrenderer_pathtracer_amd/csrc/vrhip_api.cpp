@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <array>
 #include <queue>
@@ -76,16 +77,33 @@ struct vrhip_ctx {
     // path groups per pixel (0: automatic) and their result scratch
     uint32_t path_split = 0;
     uint32_t cu_count = 256;
-    vr4* paths = nullptr;
-    size_t paths_cap = 0;        // float4 elements
+    // Render launches alternate between two path streams (parity 0/1), each
+    // with its own scratch, so a launch's paths can start while the previous
+    // launch drains; finish passes stay in order on `stream` (see render_impl)
+    struct Lane {
+        hipStream_t s = nullptr;
+        vr4* paths = nullptr;
+        size_t paths_cap = 0;        // float4 elements
+        vr4* prim = nullptr;         // primary hits, 2 float4 per owned pixel
+        size_t prim_cap = 0;         // float4 elements
+        uint32_t* chunk_ctr = nullptr;   // wave kernel work queue heads
+        hipEvent_t done = nullptr;   // recorded on `s` after the render kernels
+        hipEvent_t finished = nullptr;   // recorded on `stream` after the finish pass that read this scratch
+        bool used = false;
+    } lane[2];
+    uint32_t parity = 0;
+    bool join = true;            // the next launches must wait for everything queued on `stream`
+    hipEvent_t ev_join = nullptr;
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::vector<hipEvent_t> kev; // render-kernel start/stop pairs of the last render
-    uint32_t kev_pairs = 0;
+    // render-kernel start/stop event pairs not yet added to the totals (read
+    // without blocking at the next render, all of them by vrhip_kernel_stats),
+    // and recycled events
+    std::deque<std::pair<hipEvent_t, hipEvent_t>> kev_pending;
+    std::vector<hipEvent_t> kev_free;
     bool timed = false;          // ev0/ev1 hold the last render
-    bool pending = false;        // last render's time not yet added to the totals
     double kernel_ms_total = 0.0;
-    uint64_t launches_total = 0, launches_pending = 0;
+    uint64_t launches_total = 0;
     unsigned long long* counters = nullptr;
     // GL interop (colour, depth textures registered by the display host)
     hipGraphicsResource_t gl_res[2] = { nullptr, nullptr };
@@ -400,9 +418,20 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
     return true;
 }
 
+// Waits for the path streams' render kernels (they read the scene and their
+// scratch) and makes the next launches wait for all work queued on `stream`.
+// Every call that replaces device buffers or the stream goes through here.
+void quiesce(vrhip_ctx* c)
+{
+    for (auto& l : c->lane)
+        if (l.s) (void)hipStreamSynchronize(l.s);
+    c->join = true;
+}
+
 template <typename T>
 int upload(vrhip_ctx* c, T*& dst, const void* src, size_t bytes)
 {
+    quiesce(c);
     dfree(dst);
     HIP_TRY(hipMalloc((void**)&dst, bytes ? bytes : 16));
     if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
@@ -443,6 +472,14 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(VRHIP_ERR_HIP, "hipStreamCreate failed"));
     c->stream = c->own_stream;
+    for (auto& l : c->lane) {
+        if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&l.finished, hipEventDisableTiming) != hipSuccess)
+            return cleanup(fail(VRHIP_ERR_HIP, "path stream setup failed"));
+    }
+    if (hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+        return cleanup(fail(VRHIP_ERR_HIP, "hipEventCreate failed"));
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         c->cu_count = (uint32_t)cus;
@@ -467,15 +504,24 @@ int vrhip_destroy(vrhip_ctx* c)
     if (!c) return VRHIP_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    quiesce(c);
     dfree(c->accum); dfree(c->rgba); dfree(c->depth);
     dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     for (int i = 0; i < 2; ++i)
         if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
-    dfree(c->counters); dfree(c->paths);
+    dfree(c->counters);
+    for (auto& l : c->lane) {
+        dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr);
+        if (l.done) (void)hipEventDestroy(l.done);
+        if (l.finished) (void)hipEventDestroy(l.finished);
+        if (l.s) (void)hipStreamDestroy(l.s);
+    }
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
+    for (auto& pr : c->kev_pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (hipEvent_t e : c->kev_free) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return VRHIP_OK;
@@ -484,6 +530,7 @@ int vrhip_destroy(vrhip_ctx* c)
 int vrhip_set_stream(vrhip_ctx* c, void* s)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    quiesce(c);
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return VRHIP_OK;
 }
@@ -582,6 +629,7 @@ int vrhip_upload_hdr_half(vrhip_ctx* c, const uint16_t* rgba_half, uint32_t w, u
     const size_t n = (size_t)w * h;
     uint16_t* tmp = nullptr;
     HIP_TRY(hipMalloc((void**)&tmp, n * 8));
+    quiesce(c);
     dfree(c->hdr);
     if (hipMalloc((void**)&c->hdr, n * 16) != hipSuccess) { dfree(tmp); return fail(VRHIP_ERR_NOMEM, "hdr alloc"); }
     HIP_TRY(hipMemcpyAsync(tmp, rgba_half, n * 8, hipMemcpyHostToDevice, c->stream));
@@ -680,7 +728,11 @@ int vrhip_gl_present(vrhip_ctx* c)
     return VRHIP_OK;
 }
 
+#ifdef VR_WAVE_TIMES
+constexpr int kDebugSlots = 16 + 3 * 8192;   // + per-wave start / end / paths of render_wave_kernel
+#else
 constexpr int kDebugSlots = 16;
+#endif
 
 static int ensure_counters(vrhip_ctx* c)
 {
@@ -691,18 +743,35 @@ static int ensure_counters(vrhip_ctx* c)
     return VRHIP_OK;
 }
 
-static int account_pending(vrhip_ctx* c)
+// Adds the render-kernel times of completed launches to the totals; with
+// `wait`, waits for all of them.  Never blocks otherwise, so a render call
+// does not wait for the previous one (launches pipeline, see render_impl).
+static int account_pending(vrhip_ctx* c, bool wait)
 {
-    if (!c->pending) return VRHIP_OK;
-    HIP_TRY(hipEventSynchronize(c->ev1));
-    for (uint32_t i = 0; i < c->kev_pairs; ++i) {   // render kernel only (finish passes excluded)
+    while (!c->kev_pending.empty()) {
+        auto pr = c->kev_pending.front();
+        if (wait) {
+            HIP_TRY(hipEventSynchronize(pr.second));
+        } else {
+            const hipError_t q = hipEventQuery(pr.second);
+            if (q == hipErrorNotReady) break;
+            if (q != hipSuccess) return fail(VRHIP_ERR_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+        }
         float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, c->kev[2 * i], c->kev[2 * i + 1]));
+        HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
         c->kernel_ms_total += ms;
+        c->launches_total += 1;
+        c->kev_pending.pop_front();
+        c->kev_free.push_back(pr.first);
+        c->kev_free.push_back(pr.second);
     }
-    c->launches_total += c->launches_pending;
-    c->pending = false;
-    c->launches_pending = 0;
+    return VRHIP_OK;
+}
+
+static int take_event(vrhip_ctx* c, hipEvent_t* e)
+{
+    if (!c->kev_free.empty()) { *e = c->kev_free.back(); c->kev_free.pop_back(); return VRHIP_OK; }
+    HIP_TRY(hipEventCreate(e));
     return VRHIP_OK;
 }
 
@@ -772,34 +841,52 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
         p.counters = c->counters;
     }
-#if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS)
+#if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS) || defined(VR_WAVE_TIMES)
     if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
     p.counters = c->counters;   // diagnostic build: phase timers in slots 8..13
 #endif
-    if ((rc = account_pending(c)) != VRHIP_OK) return rc;
+    if ((rc = account_pending(c, false)) != VRHIP_OK) return rc;
     const uint32_t k_max = std::min<uint32_t>(n_frames, (uint32_t)vr::kMaxFramesPerLaunch);
     const uint32_t split_max = count ? 1u : choose_split(c, n_tiles, k_max);
     p.path_stride = n_tiles * (uint32_t)vr::kBlockThreads;
     p.use_scratch = count ? 0u : 1u;   // the counting variant accumulates in place
     if (p.use_scratch) {
         const size_t need = (size_t)2 * k_max * p.path_stride;
-        if (need > c->paths_cap) {
-            dfree(c->paths);
-            c->paths_cap = 0;
-            HIP_TRY(hipMalloc((void**)&c->paths, need * sizeof(vr4)));
-            c->paths_cap = need;
+        for (auto& l : c->lane) {
+            if (need > l.paths_cap || 2 * (size_t)p.path_stride > l.prim_cap) {
+                quiesce(c);                               // the finish passes read the scratch too
+                HIP_TRY(hipStreamSynchronize(c->stream));
+            }
+            if (need > l.paths_cap) {
+                dfree(l.paths);
+                l.paths_cap = 0;
+                HIP_TRY(hipMalloc((void**)&l.paths, need * sizeof(vr4)));
+                l.paths_cap = need;
+            }
+            if (2 * (size_t)p.path_stride > l.prim_cap) {
+                dfree(l.prim);
+                l.prim_cap = 0;
+                HIP_TRY(hipMalloc((void**)&l.prim, 2 * (size_t)p.path_stride * sizeof(vr4)));
+                l.prim_cap = 2 * (size_t)p.path_stride;
+            }
+            if (!l.chunk_ctr) {
+                const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * VR_QUEUES;
+                HIP_TRY(hipMalloc((void**)&l.chunk_ctr, bytes));
+                HIP_TRY(hipMemsetAsync(l.chunk_ctr, 0, bytes, c->stream));
+                c->join = true;
+            }
         }
-        p.paths = c->paths;
+        // the path-pool kernel is persistent: one resident set of blocks
+        // (4 per CU at 4 waves/SIMD) draining a work queue
+        p.wave_blocks = c->cu_count * 4u;
     }
-    const uint32_t iters = (n_frames + vr::kMaxFramesPerLaunch - 1) / vr::kMaxFramesPerLaunch;
-    while (c->kev.size() < 2 * (size_t)iters) {
-        hipEvent_t e = nullptr;
-        HIP_TRY(hipEventCreate(&e));
-        c->kev.push_back(e);
-    }
-    c->kev_pairs = 0;
     (void)hipGetLastError();            // launches below report their own errors only
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    if (p.use_scratch && c->join) {     // scene, stream or buffers changed: wait for all of `stream`
+        HIP_TRY(hipEventRecord(c->ev_join, c->stream));
+        for (auto& l : c->lane) HIP_TRY(hipStreamWaitEvent(l.s, c->ev_join, 0));
+        c->join = false;
+    }
     uint32_t done = 0;
     while (done < n_frames) {
         const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
@@ -807,20 +894,42 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         p.n_frames = k;
         p.split = std::min<uint32_t>(split_max, 2u * k);
         for (uint32_t i = 0; i < k; ++i) p.times[i] = times ? times[done + i] : time_seed;
-        HIP_TRY(hipEventRecord(c->kev[2 * c->kev_pairs], c->stream));
-        int e = vr::launch_render(p, n_tiles, stack, count, c->stream);
+        // Path launches run on the two path streams in turn: launch i's render
+        // kernels wait only for the finish pass of launch i-2 (the last reader
+        // of the same scratch), so they start while launch i-1 drains its
+        // longest paths; the finish passes run in order on `stream`.  The
+        // counting variant accumulates in place on `stream`.
+        auto& l = c->lane[c->parity];
+        hipStream_t rs = p.use_scratch ? l.s : c->stream;
+        if (p.use_scratch) {
+            c->parity ^= 1u;
+            p.paths = l.paths; p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
+            if (l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
+        }
+        hipEvent_t k0 = nullptr, k1 = nullptr;
+        if (n_tiles) {
+            if ((rc = take_event(c, &k0)) != VRHIP_OK || (rc = take_event(c, &k1)) != VRHIP_OK) return rc;
+            c->kev_pending.emplace_back(k0, k1);
+            HIP_TRY(hipEventRecord(k0, rs));
+        }
+        int e = vr::launch_render(p, n_tiles, stack, count, rs);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
-        HIP_TRY(hipEventRecord(c->kev[2 * c->kev_pairs + 1], c->stream));
-        ++c->kev_pairs;
+        if (n_tiles) HIP_TRY(hipEventRecord(k1, rs));
+        if (p.use_scratch) {
+            HIP_TRY(hipEventRecord(l.done, rs));
+            HIP_TRY(hipStreamWaitEvent(c->stream, l.done, 0));
+        }
         e = vr::launch_finish(p, n_tiles, c->stream);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("finish launch: ") + hipGetErrorString((hipError_t)e));
+        if (p.use_scratch) {
+            HIP_TRY(hipEventRecord(l.finished, c->stream));
+            l.used = true;
+        }
         c->frame += k;
         done += k;
-        c->launches_pending += n_tiles ? 1 : 0;
     }
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
-    c->pending = true;
     return VRHIP_OK;
 }
 
@@ -847,19 +956,32 @@ int vrhip_debug_counters(vrhip_ctx* c, uint64_t out[16], int reset)
     if (!c || !out) return fail(VRHIP_ERR_INVALID, "null argument");
     int rc = set_device(c); if (rc) return rc;
     if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
-    unsigned long long h[kDebugSlots] = {};
+    unsigned long long h[16] = {};
     HIP_TRY(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    for (int i = 0; i < kDebugSlots; ++i) out[i] = (uint64_t)h[i];
-    if (reset) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(h), c->stream));
+    for (int i = 0; i < 16; ++i) out[i] = (uint64_t)h[i];
+    if (reset) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kDebugSlots, c->stream));
     return VRHIP_OK;
 }
+
+#ifdef VR_WAVE_TIMES
+// diagnostic build only (not in vrhip.h): per-wave start, end, paths of the last wave-kernel launch
+extern "C" int vrhip_debug_wave_times(vrhip_ctx* c, uint64_t* out, uint32_t n_waves)
+{
+    if (!c || !out || n_waves > 8192) return fail(VRHIP_ERR_INVALID, "bad argument");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->counters + 16, sizeof(uint64_t) * 3 * n_waves, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return VRHIP_OK;
+}
+#endif
 
 int vrhip_kernel_stats(vrhip_ctx* c, double* total_ms, uint64_t* launches, int reset)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     int rc = set_device(c); if (rc) return rc;
-    if ((rc = account_pending(c)) != VRHIP_OK) return rc;
+    if ((rc = account_pending(c, true)) != VRHIP_OK) return rc;
     if (total_ms) *total_ms = c->kernel_ms_total;
     if (launches) *launches = c->launches_total;
     if (reset) { c->kernel_ms_total = 0.0; c->launches_total = 0; }
@@ -906,6 +1028,7 @@ int vrhip_device_buffers(vrhip_ctx* c, void** accum, void** rgba8, void** depth8
 int vrhip_set_tiling(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks)
 {
     if (!c || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad tiling");
+    quiesce(c);
     c->rank = rank; c->nranks = n_ranks;
     return VRHIP_OK;
 }
@@ -972,6 +1095,7 @@ int vrhip_last_kernel_ms(vrhip_ctx* c, float* ms)
 {
     if (!c || !ms) return fail(VRHIP_ERR_INVALID, "null argument");
     if (!c->timed) { *ms = 0.f; return VRHIP_OK; }
+    HIP_TRY(hipEventSynchronize(c->ev1));
     HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
     return VRHIP_OK;
 }
