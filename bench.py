@@ -16,10 +16,11 @@ RCCL gather (torch.distributed over "nccl" = RCCL) of the RGBA8 tiles to rank
 Strong scaling: the frame size is fixed.
 
 Prints ONE JSON line (rank 0).  value = total paths of all ranks / max-over-
-ranks wall time of the K timed steps.  roofline = the render kernel's
-algorithmic bytes per launch (counted by the kernel's counting variant on a
-separate, untimed step; SURVEY.md 8d byte costs) / its average launch time
-(HIP events on the render stream, inside the timed region).  cpu_baseline =
+ranks wall time of the K timed steps.  roofline = the render
+kernels' algorithmic bytes per launch (counted by the kernel's counting
+variant on a separate, untimed step; SURVEY.md 8d byte costs) / their
+average launch time (HIP events around primary_kernel + render_wave_kernel
+on the path stream they run on, inside the timed region).  cpu_baseline =
 the CPU oracle (oracle/, a C restatement of the reference kernel) on a
 bounded sample of the same workload on this host's cores.
 """
@@ -204,8 +205,12 @@ def main():
             "bytes_per_path": round(bytes_per_launch / max(own_paths, 1), 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "render_wave_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                         "launches": launches},
+                         "kernel": "primary_kernel+render_wave_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "launches": launches,
+                         "note": "algorithmic bytes of the reference algorithm (SURVEY 8d), served mostly from "
+                                 "L2/LDS (traffic = physical HBM bytes per launch); consecutive launches overlap on "
+                                 "two path streams, so avg_launch_ms includes time shared with the neighbouring "
+                                 "launch"},
         }
         if not args.no_cpu and world == 1:
             threads = min(16, os.cpu_count() or 1)

@@ -23,13 +23,14 @@ import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = r"render_(wave_|block_)?kernel|primary_kernel"   # one render launch = primary_kernel + render_wave_kernel
 
 
 def pmc_means(d):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if re.search(r"render_(wave_|block_)?kernel", row["Kernel_Name"]) and "true" not in row["Kernel_Name"]:
+            if re.search(KERNELS, row["Kernel_Name"]) and "true" not in row["Kernel_Name"]:
                 vals[(row["Kernel_Name"], row["Counter_Name"])].append(float(row["Counter_Value"]))
     return {f"{k[0]}|{k[1]}": sum(v) / len(v) for k, v in vals.items()}
 
@@ -46,16 +47,18 @@ def main():
     for sub in ("prof_fetch", "prof_write", "prof_sq"):
         pmc.update(pmc_means(os.path.join(src, sub)))
     json.dump(pmc, open(os.path.join(prof, f"{name}_pmc.json"), "w"), indent=1, sort_keys=True)
-    kern = [r for r in rows if re.search(r"render_(wave_|block_)?kernel", r["Name"]) and "true" not in r["Name"]]
-    fetch = [v for k, v in pmc.items() if k.endswith("|FETCH_SIZE")]
-    write = [v for k, v in pmc.items() if k.endswith("|WRITE_SIZE")]
+    kern = [r for r in rows if re.search(KERNELS, r["Name"]) and "true" not in r["Name"]]
+    launch_ms = sum(float(r["AverageNs"]) for r in kern) / 1e6
+    # per render launch: sum over its kernels (primary pass + path kernel)
+    fetch = sum(v for k, v in pmc.items() if k.endswith("|FETCH_SIZE"))
+    write = sum(v for k, v in pmc.items() if k.endswith("|WRITE_SIZE"))
     traffic = None
     if fetch and write:
-        traffic = int((2 * fetch[0] + write[0]) * 1024)
-        json.dump({"hbm_bytes_per_launch": traffic, "fetch_size_kib": fetch[0], "write_size_kib": write[0],
+        traffic = int((2 * fetch + write) * 1024)
+        json.dump({"hbm_bytes_per_launch": traffic, "fetch_size_kib": fetch, "write_size_kib": write,
                    "source": f"profiles/{name}_pmc.json", "note": "2*FETCH_SIZE+WRITE_SIZE (KiB->B) per render "
-                   "launch of bench.py's C2 step; FETCH doubling per MI355X_MICROARCH.md HBM section; WRITE is "
-                   "dominated by the split launch's 16 B/path result scratch"},
+                   "launch (primary_kernel + render_wave_kernel) of bench.py's C2 step; FETCH doubling per "
+                   "MI355X_MICROARCH.md HBM section; WRITE is dominated by the 16 B/path result scratch"},
                   open(os.path.join(prof, "traffic_c2.json"), "w"), indent=1)
     bench = ""
     blog = os.path.join(src, "bench.log")
@@ -68,10 +71,13 @@ def main():
                 f"{fps} frames per launch).\n\n## rocprofv3 --kernel-trace --stats\n\n| kernel | calls | avg ms |\n|---|---|---|\n")
         for r in rows:
             f.write(f"| `{r['Name'][:70]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} |\n")
-        f.write("\n## PMC (render kernel, per dispatch)\n\n")
+        if kern:
+            f.write(f"\nRender launch = {' + '.join(r['Name'].split('(')[0].split('::')[-1] for r in kern)}: "
+                    f"{launch_ms:.3f} ms (sum of the averages; compare bench.py roofline.avg_launch_ms)\n")
+        f.write("\n## PMC (render kernels, per dispatch)\n\n")
         for k, v in sorted(pmc.items()):
-            f.write(f"- {k.split('|')[1]}: {v:.4g}\n")
-        sq = {k.split('|')[1]: v for k, v in pmc.items()}
+            f.write(f"- {k.split('|')[0].split('(')[0].split('::')[-1]} {k.split('|')[1]}: {v:.4g}\n")
+        sq = {k.split('|')[1]: v for k, v in pmc.items() if "render_wave_kernel" in k}
         if "SQ_THREAD_CYCLES_VALU" in sq and "SQ_ACTIVE_INST_VALU" in sq:
             f.write(f"\nVALU lane utilisation = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU) = "
                     f"{sq['SQ_THREAD_CYCLES_VALU'] / (64 * sq['SQ_ACTIVE_INST_VALU']):.3f}\n")

@@ -240,17 +240,18 @@ def test_pipelined_steps_bitexact_vs_portable_oracle(native, oracle):
         assert_bitexact(g, o, sc, what)
 
 
-@pytest.mark.parametrize("cfg", ["C3", "C4"])
-def test_pipelined_steps_with_scene_changes_equal_synchronous(native, cfg):
+@pytest.mark.parametrize("cfg,overlap", [("C3", 1), ("C4", 1), ("C3", 0)])
+def test_pipelined_steps_with_scene_changes_equal_synchronous(native, cfg, overlap):
     """Uploads, Fresnel and tiling changes between unsynchronised render calls
     take effect exactly where they were issued (the path streams join the
-    render stream after any buffer change)."""
+    render stream after any buffer change), with and without launch overlap."""
     sc = scenes.make_scene(cfg, 96, 64)
     t = sc["time"]
 
     def run(sync):
         r = VRendererHIP(0)
         scenes.load_into(r, sc)
+        r.set_overlap(overlap)
         r.render(frames=2, times=[t, t + 1], sync=sync)
         r.render(frames=3, times=[t + 2, t + 3, t + 4], sync=sync)
         r.loadHDR(np.ascontiguousarray(sc["hdr"][::-1]))

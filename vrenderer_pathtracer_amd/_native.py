@@ -64,6 +64,7 @@ _SIGNATURES = {
     "vrhip_debug_counters": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "vrhip_sync": (ctypes.c_int, [_ctx]),
     "vrhip_set_path_split": (ctypes.c_int, [_ctx, ctypes.c_uint32]),
+    "vrhip_set_overlap": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "vrhip_frame_count": (ctypes.c_int, [_ctx, _u32]),
     "vrhip_read_accum": (ctypes.c_int, [_ctx, _f]),
     "vrhip_read_rgba8": (ctypes.c_int, [_ctx, _u8]),

@@ -92,6 +92,7 @@ struct vrhip_ctx {
         bool used = false;
     } lane[2];
     uint32_t parity = 0;
+    int overlap = -1;            // vrhip_set_overlap: 1 always, 0 never, -1 small launches only
     bool join = true;            // the next launches must wait for everything queued on `stream`
     hipEvent_t ev_join = nullptr;
     // timing
@@ -899,10 +900,14 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // of the same scratch), so they start while launch i-1 drains its
         // longest paths; the finish passes run in order on `stream`.  The
         // counting variant accumulates in place on `stream`.
+        // Without overlap every launch uses the same path stream, so it waits
+        // for the previous one (and its finish pass, below) like a single stream.
+        const bool ovl = c->overlap > 0 || (c->overlap < 0 && (size_t)p.path_stride * 2u * k < ((size_t)1 << 24));
+        if (!ovl) c->parity = 0;
         auto& l = c->lane[c->parity];
         hipStream_t rs = p.use_scratch ? l.s : c->stream;
         if (p.use_scratch) {
-            c->parity ^= 1u;
+            if (ovl) c->parity ^= 1u;
             p.paths = l.paths; p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
             if (l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
         }
@@ -1030,6 +1035,13 @@ int vrhip_set_tiling(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks)
     if (!c || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad tiling");
     quiesce(c);
     c->rank = rank; c->nranks = n_ranks;
+    return VRHIP_OK;
+}
+
+int vrhip_set_overlap(vrhip_ctx* c, int mode)
+{
+    if (!c || mode < -1 || mode > 1) return fail(VRHIP_ERR_INVALID, "bad overlap mode");
+    c->overlap = mode;
     return VRHIP_OK;
 }
 

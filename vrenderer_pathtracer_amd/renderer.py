@@ -311,6 +311,10 @@ class VRendererHIP:
         """Path groups per pixel per launch (0 = automatic, 1 = off); results are unchanged."""
         check(self._lib.vrhip_set_path_split(self._need_ctx(), groups), "vrhip_set_path_split")
 
+    def set_overlap(self, mode: int) -> None:
+        """Overlap of consecutive render launches: 1 always, 0 never, -1 automatic (vrhip_set_overlap)."""
+        check(self._lib.vrhip_set_overlap(self._need_ctx(), int(mode)), "vrhip_set_overlap")
+
     def owned_pixels(self) -> int:
         """Pixels this rank renders (256 per owned 16x16 tile)."""
         n = ctypes.c_uint32(0)
