@@ -144,8 +144,12 @@ int vrhip_gl_present(vrhip_ctx *ctx);
  * cu_runRenderKernel (cuda/src/PathTracer.cu:870-892), for n_frames
  * consecutive frames in one device pass.  times[i] is the _time RNG seed of
  * frame i (the reference uses wall-clock ms); times may be NULL, then
- * `time_seed` is used for every frame.  Enqueues on the context stream and
- * returns; call vrhip_sync for the reference's synchronous behaviour. */
+ * `time_seed` is used for every frame.  Enqueues and returns; call
+ * vrhip_sync for the reference's synchronous behaviour.  The path kernels
+ * run on the context's two internal path streams (see vrhip_set_overlap);
+ * the finish pass that writes the accumulation, colour and depth images runs
+ * on the context stream after them, so work queued on the context stream
+ * afterwards (reads, vrhip_pack_tiles, a collective) sees the results. */
 int vrhip_render(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed);
 /* Same render, through the counting kernel variant (identical results, plus
  * per-event counts for the roofline's algorithmic bytes):
