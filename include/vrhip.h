@@ -161,13 +161,13 @@ int vrhip_render(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint3
 int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
                          uint64_t counters[8]);
 int vrhip_sync(vrhip_ctx *ctx);
-/* Path groups per pixel for vrhip_render (no reference counterpart: a launch
- * shape knob).  A launch of k frames has 2k paths per pixel; with groups > 1
- * they are split into that many contiguous runs on different workgroups and
- * summed in path order afterwards, so results are unchanged.  0 (default)
- * picks the smallest power of two that gives every CU enough workgroups
- * (matters for small images and multi-GPU band shards); 1 disables the
- * split.  At most 128. */
+/* Path groups per pixel for vrhip_render in sphere-only scenes (no
+ * reference counterpart: a launch shape knob; mesh scenes use the persistent
+ * path kernel, whose work queues need none).  A launch of k frames has 2k
+ * paths per pixel; with groups > 1 they are split into that many contiguous
+ * runs on different workgroups and summed in path order afterwards, so
+ * results are unchanged.  0 (default) picks the smallest power of two that
+ * gives every CU enough workgroups; 1 disables the split.  At most 128. */
 int vrhip_set_path_split(vrhip_ctx *ctx, uint32_t groups);
 /* Overlap of consecutive render launches (no reference counterpart: a
  * scheduling knob; results are unchanged).  The path kernels of launch i+1
@@ -217,8 +217,11 @@ int vrhip_unpack_tiles(vrhip_ctx *ctx, int what, const void *src_device, uint32_
  * requires vrhip_sync first). */
 int vrhip_last_kernel_ms(vrhip_ctx *ctx, float *ms);
 /* Accumulated render-kernel time (ms) and launch count since the last reset,
- * from HIP events recorded around every render-kernel launch on the context
- * stream (the split passes' finish kernel is not included). */
+ * from HIP events recorded around every launch's render kernels
+ * (primary_kernel + render_wave_kernel, or render_kernel) on the stream they
+ * run on; the finish pass is not included.  With launch overlap a launch's
+ * span includes time shared with the neighbouring launch.  Waits for the
+ * pending launches. */
 int vrhip_kernel_stats(vrhip_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
 /* Raw debug slots: [0..7] the last counted render's counters; [8..13] phase
  * cycle totals (spheres, mesh traversal, hit materialisation, shading,
