@@ -463,23 +463,16 @@ __device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, 
 // the closest-hit update (:379-386).  Evaluated branch-free: every early
 // return of the reference becomes a term of the final predicate (the values
 // computed for a surviving triangle are the same operations in the same order).
+struct TriV { vr3 a0, a1, a2; };
 template <bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Trav& tr, int k, Cnt& cnt)
+__device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, Trav& tr, int k, const TriV& t, Cnt& cnt)
 {
-#ifdef VR_DROP_TRIS
-    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, 0u);     // timing probe: loads return 0
-#else
-    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, p.n_tris * 36u);
-#endif
     const bool strict = HAS(F_STRICT);
     if (COUNT) cnt.tris++;
     VR_LANE(2, 3);
-    const int toff = k * 36;
-    const vr3 a0 = buf_load3(tbuf, toff), a1 = buf_load3(tbuf, toff + 12), a2 = buf_load3(tbuf, toff + 24);
-    asm volatile("" ::"v"(a0.x), "v"(a1.x), "v"(a2.x));   // three dwordx3 loads, one trip
-    const vr4 v0 = mk4(a0.x, a0.y, a0.z, 0.f);
-    const vr4 v1 = mk4(a1.x, a1.y, a1.z, 0.f);
-    const vr4 v2 = mk4(a2.x, a2.y, a2.z, 0.f);
+    const vr4 v0 = mk4(t.a0.x, t.a0.y, t.a0.z, 0.f);
+    const vr4 v1 = mk4(t.a1.x, t.a1.y, t.a1.z, 0.f);
+    const vr4 v2 = mk4(t.a2.x, t.a2.y, t.a2.z, 0.f);
     const vr4 e1 = sub4(v1, v0), e2 = sub4(v2, v0);
     const vr4 pv = cross4(r.d, e2);
     const float det = dot4(e1, pv);
@@ -497,12 +490,34 @@ __device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Tr
     }
 }
 
+__device__ __forceinline__ TriV tri_load(const RenderParams& p, int k)
+{
+#ifdef VR_DROP_TRIS
+    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, 0u);     // timing probe: loads return 0
+#else
+    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, p.n_tris * 36u);
+#endif
+    const int toff = k * 36;
+    TriV t;
+    t.a0 = buf_load3(tbuf, toff); t.a1 = buf_load3(tbuf, toff + 12); t.a2 = buf_load3(tbuf, toff + 24);
+    return t;
+}
+
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Trav& tr, int k, Cnt& cnt)
+{
+    const TriV t = tri_load(p, k);
+    asm volatile("" ::"v"(t.a0.x), "v"(t.a1.x), "v"(t.a2.x));   // three dwordx3 loads, one trip
+    tri_test_v<COUNT, FEAT>(p, r, tr, k, t, cnt);
+}
+
 // One outer iteration of the while-while loop: the inner node loop until
 // this lane holds a leaf and the wave agrees (ballot, :353-363), with one
 // leaf postponed (:345-351), then the leaf loop.  Precondition: tr.nodeAddr
 // is an inner node (not kSentinel).
 #ifndef VR_NODE_BREAK
-#define VR_NODE_BREAK 2    // measured: C2 +5 %, C3 +3 % over 0 (the reference's all-lanes vote)
+#define VR_NODE_BREAK 6    // measured (path kernel with paired triangle loads): 0 (the reference's
+                           // all-lanes vote) C2 2,294, 2: 2,503, 4: 2,563, 6: 2,577, 8: 2,583 (C3 -2 %)
 #endif
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
@@ -523,7 +538,19 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
     while (leafAddr < 0) {
         const int lv = ~leafAddr;
         const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
+#ifndef VR_NO_TRI_PAIRS
+        // the loads of two triangles in one trip (the tests stay in slot order):
+        // a leaf's triangles need half the dependent round trips (C2 +1 %, C3 +4 %)
+        for (int k = lv >> kLeafCountBits; k < kend; k += 2) {
+            const bool two = k + 1 < kend;
+            const TriV ta = tri_load(p, k), tb = tri_load(p, two ? k + 1 : k);
+            asm volatile("" ::"v"(ta.a0.x), "v"(ta.a1.x), "v"(ta.a2.x), "v"(tb.a0.x), "v"(tb.a1.x), "v"(tb.a2.x));
+            tri_test_v<COUNT, FEAT>(p, r, tr, k, ta, cnt);
+            if (two) tri_test_v<COUNT, FEAT>(p, r, tr, k + 1, tb, cnt);
+        }
+#else
         for (int k = lv >> kLeafCountBits; k < kend; ++k) tri_test<COUNT, FEAT>(p, r, tr, k, cnt);
+#endif
         leafAddr = tr.nodeAddr;
         if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop(tr, stk);
     }
