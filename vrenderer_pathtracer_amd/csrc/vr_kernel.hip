@@ -177,9 +177,9 @@ constexpr int kLeafCountBits = 7;
 #define VR_LDS_BUDGET (40960 - 256)
 #endif
 constexpr int kLdsBudget = VR_LDS_BUDGET;
-constexpr int cache_nodes(int stack, int extra = 0) {
-    return (kLdsBudget - stack * kBlockThreads * 4 - extra) / 56 > 0 ?
-           (kLdsBudget - stack * kBlockThreads * 4 - extra) / 56 : 1;
+constexpr int cache_nodes(int stack, int extra = 0, int bt = kBlockThreads) {
+    return ((bt / kBlockThreads) * kLdsBudget - stack * bt * 4 - extra) / 56 > 0 ?
+           ((bt / kBlockThreads) * kLdsBudget - stack * bt * 4 - extra) / 56 : 1;
 }
 // Raw buffer loads for the node and triangle arrays: a 32-bit lane offset
 // against an SGPR descriptor (bounds-checked, no 64-bit address math), and an
@@ -226,6 +226,7 @@ struct Lds {
     const vr4* nodes;         // fp32 nodes: 3 rows per cached node; fp16 nodes: 2 rows per node
     const int2* idx;          // fp32 nodes: child indices per cached node
     int n_cached;             // nodes [0, n_cached) are read from LDS
+    int stride;               // stack entry stride (threads per block; entry-major [depth][threads])
 };
 
 // CudaTracerLib-style while-while traversal (PathTracer.cu:276-463), split
@@ -269,15 +270,15 @@ __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, f
 // Pop (:339-342 and the leaf-loop pops): the top is already in a register;
 // the entry below it is read for the next pop, off the critical path.  sp
 // reaches -1 only by popping the sentinel, after which nothing is popped.
-__device__ __forceinline__ int trav_pop(Trav& tr, const int* stk)
+__device__ __forceinline__ int trav_pop(Trav& tr, const Lds& L)
 {
 #ifdef VR_TOP_IN_REG
     const int v = tr.top;
     --tr.sp;
-    tr.top = stk[(tr.sp > 0 ? tr.sp : 0) * kBlockThreads];
+    tr.top = L.stk[(tr.sp > 0 ? tr.sp : 0) * L.stride];
     return v;
 #else
-    return stk[(tr.sp--) * kBlockThreads];
+    return L.stk[(tr.sp--) * L.stride];
 #endif
 }
 
@@ -391,14 +392,14 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     // branch-free, stack top in a register: the entry below the new top is
     // read every visit but only consumed by a later pop
     const int popped = tr.top;
-    if (both) stk[(tr.sp + 1) * kBlockThreads] = farc;
+    if (both) stk[(tr.sp + 1) * L.stride] = farc;
     tr.sp += both ? 1 : (none ? -1 : 0);
     tr.nodeAddr = none ? popped : nearc;
-    const int below = stk[(tr.sp > 0 ? tr.sp : 0) * kBlockThreads];
+    const int below = stk[(tr.sp > 0 ? tr.sp : 0) * L.stride];
     tr.top = both ? farc : (none ? below : tr.top);
 #else
-    const int top = stk[tr.sp * kBlockThreads];
-    if (both) stk[(tr.sp + 1) * kBlockThreads] = farc;
+    const int top = stk[tr.sp * L.stride];
+    if (both) stk[(tr.sp + 1) * L.stride] = farc;
     tr.sp += both ? 1 : (none ? -1 : 0);
     tr.nodeAddr = none ? top : nearc;
 #endif
@@ -449,12 +450,12 @@ __device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, 
         val[i] = sw ? vj : vi; val[j] = sw ? vi : vj;
     };
     cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
-    const int top = stk[tr.sp * kBlockThreads];
-    if (n >= 4) stk[(tr.sp + 1) * kBlockThreads] = val[3];
+    const int top = stk[tr.sp * L.stride];
+    if (n >= 4) stk[(tr.sp + 1) * L.stride] = val[3];
     tr.sp += n >= 4 ? 1 : 0;
-    if (n >= 3) stk[(tr.sp + 1) * kBlockThreads] = val[2];
+    if (n >= 3) stk[(tr.sp + 1) * L.stride] = val[2];
     tr.sp += n >= 3 ? 1 : 0;
-    if (n >= 2) stk[(tr.sp + 1) * kBlockThreads] = val[1];
+    if (n >= 2) stk[(tr.sp + 1) * L.stride] = val[1];
     tr.sp += n >= 2 ? 1 : (n == 0 ? -1 : 0);
     tr.nodeAddr = n == 0 ? top : val[0];
 }
@@ -529,7 +530,7 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         else node_step<COUNT, FEAT>(p, r, tr, L, cnt);
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
             leafAddr = tr.nodeAddr;
-            tr.nodeAddr = trav_pop(tr, stk);
+            tr.nodeAddr = trav_pop(tr, L);
         }
         // the wave moves on to the leaves once (nearly) every lane holds one;
         // lanes still searching resume in the next outer iteration
@@ -552,7 +553,7 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         for (int k = lv >> kLeafCountBits; k < kend; ++k) tri_test<COUNT, FEAT>(p, r, tr, k, cnt);
 #endif
         leafAddr = tr.nodeAddr;
-        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop(tr, stk);
+        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop(tr, L);
     }
 }
 
@@ -573,7 +574,7 @@ __device__ __forceinline__ void trav_step(const RenderParams& p, const Ray& r, T
         const int lv = ~tr.nodeAddr;
         tr.k = lv >> kLeafCountBits;
         tr.kend = tr.k + (lv & ((1 << kLeafCountBits) - 1));
-        tr.nodeAddr = trav_pop(tr, L.stk);
+        tr.nodeAddr = trav_pop(tr, L);
     }
 }
 
@@ -1009,12 +1010,13 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
 
 // Binds this thread's stack column and fills the block's node cache with
 // the first nodes of the area-ordered node array.
-template <uint32_t FEAT>
+template <uint32_t FEAT, int BT = kBlockThreads>
 __device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, vr4* lds_nodes, int2* lds_idx,
                                          int cn, int tid)
 {
     Lds L;
     L.stk = lds_stack + tid;
+    L.stride = BT;
     L.nodes = lds_nodes;
     L.idx = lds_idx;
     L.n_cached = 0;
@@ -1023,11 +1025,11 @@ __device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, 
         if (kFp16Nodes && !HAS(F_STRICT)) {            // fp16 nodes, 32 B: 1.5x as many fit
             const uint32_t cap = (uint32_t)(3 * cn / 2);
             L.n_cached = (int)(p.n_nodes < cap ? p.n_nodes : cap);
-            for (int i = tid; i < 2 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh16[i];
+            for (int i = tid; i < 2 * L.n_cached; i += BT) lds_nodes[i] = p.bvh16[i];
         } else {
             L.n_cached = (int)(p.n_nodes < (uint32_t)cn ? p.n_nodes : (uint32_t)cn);
-            for (int i = tid; i < 3 * L.n_cached; i += kBlockThreads) lds_nodes[i] = p.bvh[(i / 3) * 4 + i % 3];
-            for (int i = tid; i < L.n_cached; i += kBlockThreads)
+            for (int i = tid; i < 3 * L.n_cached; i += BT) lds_nodes[i] = p.bvh[(i / 3) * 4 + i % 3];
+            for (int i = tid; i < L.n_cached; i += BT)
                 lds_idx[i] = *reinterpret_cast<const int2*>(p.bvh + 4 * i + 3);
         }
         __syncthreads();
@@ -1155,6 +1157,7 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
     const int tid = threadIdx.x;
     Lds L;
     L.stk = lds_stack + tid;
+    L.stride = kBlockThreads;
     L.nodes = nullptr;
     L.idx = nullptr;
     L.n_cached = 0;
@@ -1201,15 +1204,26 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
 #endif
 enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3 };
 
+// Block size of the path kernel: its blocks hold no tiles, so one block of
+// 1,024 threads per CU shares one LDS node cache four times the size of a
+// 256-thread block's (at the same 4 waves/SIMD).
+#ifndef VR_WAVE_BLOCK
+#define VR_WAVE_BLOCK 1024
+#endif
+static_assert(VR_WAVE_BLOCK % kBlockThreads == 0, "VR_WAVE_BLOCK must be a multiple of 256");
+// 64-entry stacks (trees deeper than 30) need 64 KB per 256 threads
+constexpr int wave_block(int stack) { return stack <= 32 ? VR_WAVE_BLOCK : kBlockThreads; }
+
 template <int STACK, uint32_t FEAT>
-__global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_wave_kernel(const RenderParams p)
+__global__ void __launch_bounds__(wave_block(STACK), VR_MIN_WAVES_PER_SIMD) render_wave_kernel(const RenderParams p)
 {
-    constexpr int CN = cache_nodes(STACK);
-    __shared__ int lds_stack[STACK * kBlockThreads];
+    constexpr int BT = wave_block(STACK);
+    constexpr int CN = cache_nodes(STACK, 0, BT);
+    __shared__ int lds_stack[STACK * BT];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
     const int tid = threadIdx.x;
-    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
+    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
     const int lane = tid & 63;
     const uint32_t n_paths = 2u * p.n_frames;
     const uint32_t n_sub = p.path_stride >> 6;             // 8x8 sub-tiles of the rank's tiles
@@ -1347,7 +1361,7 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
     }
 #ifdef VR_WAVE_TIMES
     if (p.counters && lane == 0) {   // diagnostic: per-wave start / end (100 MHz) and paths completed
-        unsigned long long* w = p.counters + 16 + 3 * (blockIdx.x * 4u + (uint32_t)(tid >> 6));
+        unsigned long long* w = p.counters + 16 + 3 * (blockIdx.x * (uint32_t)(BT / 64) + (uint32_t)(tid >> 6));
         w[0] = wt0; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = wpaths;
     }
 #endif
@@ -1365,298 +1379,6 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_w
 #endif
 }
 
-// Block-queue variant of the path-pool kernel.  Each round, every lane
-// shades its path's last hit and produces its next ray (lanes whose path
-// ended take the next item of their wave's pool); rays that must traverse
-// the mesh are pushed into a block-wide LDS queue, and then all 256 lanes of
-// the block traverse the queued rays together, each lane taking the next
-// queued ray whenever its current one is done.  The traversal no longer runs
-// at the pace of the few deep rays in one wave: it is compacted over the
-// block, and lanes with no path left still traverse other lanes' rays.
-// Results go back through the queue slots.  Every path's operations are
-// unchanged (results bit-identical).
-constexpr int kQueueBytes = 2 * 16 * kBlockThreads + 16;
-
-template <int STACK, uint32_t FEAT>
-__global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_block_kernel(const RenderParams p)
-{
-    constexpr int CN = cache_nodes(STACK, kQueueBytes);
-    __shared__ int lds_stack[STACK * kBlockThreads];
-    __shared__ vr4 lds_nodes[3 * CN];
-    __shared__ int2 lds_idx[CN];
-    __shared__ vr4 q_a[kBlockThreads];                     // (o.xyz, t0) in; (t, bu, bv, best) out
-    __shared__ vr4 q_b[kBlockThreads];                     // (d.xyz, -)
-    __shared__ int q_count, q_next;
-    const int tid = threadIdx.x;
-    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
-    const uint32_t T = p.split;
-    const uint32_t tile = blockIdx.x / T;
-    const uint32_t g = blockIdx.x - tile * T;
-    const int wave = tid >> 6, lane = tid & 63;
-    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
-    const uint32_t tile_y = gtile / p.tiles_x;
-    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
-    const uint32_t x0 = tile_x * 16u + (uint32_t)((wave & 1) * 8);
-    const uint32_t y0 = tile_y * 16u + (uint32_t)((wave >> 1) * 8);
-    const uint32_t n_paths = 2u * p.n_frames;
-    const uint32_t chunk = (n_paths + T - 1u) / T;
-    const uint32_t q0 = g * chunk < n_paths ? g * chunk : n_paths;
-    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
-    const uint32_t pool = 64u * (q1 - q0);
-    vr4* const out_base = p.paths + (size_t)tile * kBlockThreads + (size_t)wave * 64u;
-    Cnt cnt;
-
-    uint32_t item = (uint32_t)lane;
-    uint32_t next = 64u;                                   // wave-uniform: first unassigned item
-    int state = LS_DONE;
-    int my_e = 0;                                          // queue slot of this lane's ray
-    Ray ray;
-    PathState ps;
-    HitRec hr;
-    auto start = [&]() {                                   // render's per-sample prologue (:817-844)
-        const uint32_t px = item & 63u, q = q0 + (item >> 6), f = q >> 1;
-        const uint32_t x = x0 + (px & 7u), y = y0 + (px >> 3);
-        uint32_t s1 = x * (p.first_frame + f);
-        uint32_t s2 = y * p.times[f];
-        if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
-        path_begin(ps, s1, s2);
-        ray = camera_ray(p, x, y);
-        state = LS_SETUP;
-    };
-    if (item < pool) start();
-    if (tid == 0) { q_count = 0; q_next = 0; }
-    __syncthreads();
-
-    VR_T0(t_kernel);
-    for (;;) {
-        // results of the last traversal round
-        if (state == LS_TRAV) {
-            const vr4 res = q_a[my_e];
-            const int best = __float_as_int(res.w);
-            if (best >= 0) { hr.t = res.x; hr.kind = HK_MESH; hr.idx = best; hr.bu = res.y; hr.bv = res.z; }
-            state = LS_SHADE;
-        }
-        VR_T0(t_shblk);
-        bool ended = false;
-        if (state == LS_SHADE) {
-            VR_LANE(4, 5);
-            vr4 out;
-            if (bounce_step<false, FEAT>(p, ray, hr, ps, out, cnt)) {
-                out_base[(size_t)(q0 + (item >> 6)) * p.path_stride + (item & 63u)] = out;
-                ended = true;
-            } else {
-                state = LS_SETUP;
-            }
-        }
-        const unsigned long long em = __ballot(ended);
-        if (em != 0ull) {
-            if (ended) {
-                item = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-                if (item < pool) start();
-                else state = LS_DONE;
-            }
-            next += (uint32_t)__popcll(em);
-        }
-        VR_T1(t_shblk, 4);
-        VR_T0(t_setup);
-        VR_T0(t_b1);
-        __syncthreads();                                   // every result read: queue slots are free
-        VR_T1(t_b1, 2);
-        if (state == LS_SETUP) {
-            if (intersect_spheres<false, FEAT>(p, ray, hr, cnt)) {
-                my_e = atomicAdd(&q_count, 1);
-                q_a[my_e] = mk4(ray.o.x, ray.o.y, ray.o.z, hr.t);
-                q_b[my_e] = mk4(ray.d.x, ray.d.y, ray.d.z, 0.f);
-                state = LS_TRAV;
-            } else {
-                state = LS_SHADE;
-            }
-        }
-        VR_T1(t_setup, 0);
-        VR_T0(t_b2);
-        const int alive = __syncthreads_or(state != LS_DONE);
-        VR_T1(t_b2, 2);
-        if (!alive) break;
-        VR_T0(t_trav);
-        const int n_q = q_count;
-        if (n_q > 0) {
-            // cooperative traversal of the queued rays
-            bool has = false, exhausted = false;
-            int e = 0;
-            Ray r;
-            Trav tr;
-            for (;;) {
-                if (!exhausted) {
-                    const unsigned long long need = __ballot(!has);
-                    if (need != 0ull) {
-                        int base = 0;
-                        if (lane == __ffsll((long long)need) - 1) base = atomicAdd(&q_next, __popcll(need));
-                        base = __shfl(base, __ffsll((long long)need) - 1, 64);
-                        if (base + __popcll(need) >= n_q) exhausted = true;
-                        if (!has) {
-                            e = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                            if (e < n_q) {
-                                const vr4 a = q_a[e], b = q_b[e];
-                                r.o = mk4(a.x, a.y, a.z, 0.f);
-                                r.d = mk4(b.x, b.y, b.z, 0.f);
-                                trav_init<FEAT>(p, r, a.w, tr, L);
-                                has = true;
-                            }
-                        }
-                    }
-                }
-                if (__ballot(has) == 0ull) break;
-                if (has) {
-                    trav_iter<STACK, false, FEAT>(p, r, tr, L, cnt);
-                    if (tr.nodeAddr == kSentinel) {
-                        q_a[e] = mk4(tr.t, tr.bu, tr.bv, __int_as_float(tr.best));
-                        has = false;
-                    }
-                }
-            }
-        }
-        VR_T1(t_trav, 1);
-        VR_T0(t_b3);
-        __syncthreads();                                   // every result written
-        VR_T1(t_b3, 2);
-        if (tid == 0) { q_count = 0; q_next = 0; }         // read only after the next barrier
-    }
-    VR_T1(t_kernel, 5);
-#if defined(VR_LANESTATS) || defined(VR_TIMING)
-    if (p.counters) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            unsigned long long v = cnt.tm[k];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-            if (lane == 0) atomicAdd(p.counters + 8 + k, v);
-        }
-    }
-#endif
-}
-
-// Two-paths-per-lane variant of the path-pool kernel (-DVR_TWO_PATHS): each
-// lane holds two paths; it traverses one ray at a time and, when that ray's
-// traversal ends, switches at once to its other path's ray if that one is
-// waiting, so a lane idles in the traversal loop only when both its paths
-// wait for shading.
-enum SlotState : int { SS_SETUP = 0, SS_READY = 1, SS_TRAV = 2, SS_SHADE = 3, SS_DONE = 4 };
-struct Slot {
-    uint32_t item;
-    int st;
-    Ray ray;
-    PathState ps;
-    HitRec hr;
-};
-
-template <int STACK, uint32_t FEAT>
-__global__ void __launch_bounds__(kBlockThreads, 3) render_wave2_kernel(const RenderParams p)
-{
-    constexpr int CN = cache_nodes(STACK);
-    __shared__ int lds_stack[STACK * kBlockThreads];
-    __shared__ vr4 lds_nodes[3 * CN];
-    __shared__ int2 lds_idx[CN];
-    const int tid = threadIdx.x;
-    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
-    const uint32_t T = p.split;
-    const uint32_t tile = blockIdx.x / T;
-    const uint32_t g = blockIdx.x - tile * T;
-    const int wave = tid >> 6, lane = tid & 63;
-    const uint32_t gtile = p.rank + tile * p.nranks;
-    const uint32_t tile_y = gtile / p.tiles_x;
-    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
-    const uint32_t x0 = tile_x * 16u + (uint32_t)((wave & 1) * 8);
-    const uint32_t y0 = tile_y * 16u + (uint32_t)((wave >> 1) * 8);
-    const uint32_t n_paths = 2u * p.n_frames;
-    const uint32_t chunk = (n_paths + T - 1u) / T;
-    const uint32_t q0 = g * chunk < n_paths ? g * chunk : n_paths;
-    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
-    const uint32_t pool = 64u * (q1 - q0);
-    vr4* const out_base = p.paths + (size_t)tile * kBlockThreads + (size_t)wave * 64u;
-    Cnt cnt;
-
-    auto start = [&](Slot& sl) {                           // render's per-sample prologue (:817-844)
-        const uint32_t px = sl.item & 63u, q = q0 + (sl.item >> 6), f = q >> 1;
-        const uint32_t x = x0 + (px & 7u), y = y0 + (px >> 3);
-        uint32_t s1 = x * (p.first_frame + f);
-        uint32_t s2 = y * p.times[f];
-        if (q & 1u) (void)hash_seeds(s1, s2);
-        path_begin(sl.ps, s1, s2);
-        sl.ray = camera_ray(p, x, y);
-        sl.st = SS_SETUP;
-    };
-    auto setup = [&](Slot& sl) {
-        if (sl.st == SS_SETUP)
-            sl.st = intersect_spheres<false, FEAT>(p, sl.ray, sl.hr, cnt) ? SS_READY : SS_SHADE;
-    };
-    Slot sa, sb;
-    sa.item = (uint32_t)lane; sa.st = SS_DONE;
-    sb.item = 64u + (uint32_t)lane; sb.st = SS_DONE;
-    if (sa.item < pool) start(sa);
-    if (sb.item < pool) start(sb);
-    uint32_t next = 128u;                                  // wave-uniform: first unassigned item
-    int cur = -1;                                          // slot being traversed
-    Ray rt;
-    Trav tr;
-    auto try_start = [&]() {
-        if (cur < 0) {
-            if (sa.st == SS_READY) { cur = 0; sa.st = SS_TRAV; rt = sa.ray; trav_init<FEAT>(p, rt, sa.hr.t, tr, L); }
-            else if (sb.st == SS_READY) { cur = 1; sb.st = SS_TRAV; rt = sb.ray; trav_init<FEAT>(p, rt, sb.hr.t, tr, L); }
-        }
-    };
-
-    for (;;) {
-        setup(sa);
-        setup(sb);
-        try_start();
-        for (;;) {
-            const int n_trav = __popcll(__ballot(cur >= 0));
-            if (n_trav == 0) break;
-            const int n_wait = __popcll(__ballot(cur < 0 && (sa.st == SS_SHADE || sb.st == SS_SHADE)));
-            if (n_wait >= VR_SHADE_BATCH && n_wait * VR_SHADE_RATIO >= n_trav) break;
-            if (cur >= 0) {
-                trav_iter<STACK, false, FEAT>(p, rt, tr, L, cnt);
-                if (tr.nodeAddr == kSentinel) {
-                    if (cur == 0) { trav_finish(tr, sa.hr); sa.st = SS_SHADE; }
-                    else { trav_finish(tr, sb.hr); sb.st = SS_SHADE; }
-                    cur = -1;
-                    setup(sa);
-                    setup(sb);
-                    try_start();
-                }
-            }
-        }
-        auto shade = [&](Slot& sl) {
-            bool ended = false;
-            if (sl.st == SS_SHADE) {
-                vr4 out;
-                if (bounce_step<false, FEAT>(p, sl.ray, sl.hr, sl.ps, out, cnt)) {
-                    out_base[(size_t)(q0 + (sl.item >> 6)) * p.path_stride + (sl.item & 63u)] = out;
-                    ended = true;
-                } else {
-                    sl.st = SS_SETUP;
-                }
-            }
-            const unsigned long long em = __ballot(ended);
-            if (em != 0ull) {
-                if (ended) {
-                    sl.item = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-                    if (sl.item < pool) start(sl);
-                    else sl.st = SS_DONE;
-                }
-                next += (uint32_t)__popcll(em);
-            }
-        };
-        shade(sa);
-        shade(sb);
-        if (__ballot(sa.st != SS_DONE || sb.st != SS_DONE || cur >= 0) == 0ull) break;
-    }
-}
-
-// ---- small helper kernels ------------------------------------------------
 __global__ void half_to_float_kernel(const uint16_t* __restrict__ src, vr4* __restrict__ dst, size_t n)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1718,7 +1440,10 @@ template <int STACK, uint32_t FEAT>
 static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
     hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
-    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT>), dim3(p.wave_blocks), dim3(kBlockThreads), 0, s, p);
+    // p.wave_blocks counts 256-thread blocks
+    constexpr int BT = wave_block(STACK);
+    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT>), dim3(p.wave_blocks / (BT / kBlockThreads)),
+                       dim3(BT), 0, s, p);
 }
 
 template <uint32_t FEAT>
@@ -1737,22 +1462,10 @@ static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth
     const uint32_t blocks = n_tiles * p.split;
     if (!wave)
         hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-#if defined(VR_TWO_PATHS)
-    else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
-        hipLaunchKernelGGL((render_wave2_kernel<16, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-    else
-        hipLaunchKernelGGL((render_wave2_kernel<32, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-#elif defined(VR_BLOCK_QUEUE)
-    else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
-        hipLaunchKernelGGL((render_block_kernel<16, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-    else
-        hipLaunchKernelGGL((render_block_kernel<32, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-#else
     else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
         launch_wave<16, FEAT>(p, n_tiles, s);
     else
         launch_wave<32, FEAT>(p, n_tiles, s);
-#endif
 }
 
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream)
