@@ -48,6 +48,8 @@ def test_null_context_is_invalid(native):
     assert native.vrhip_clear(None) == -1
     assert native.vrhip_render(None, 1, None, 0) == -1
     assert native.vrhip_set_fresnel(None, 0.1, 3.0) == -1
+    assert native.vrhip_set_overlap(None, -1) == -1
+    assert native.vrhip_set_path_split(None, 0) == -1
     assert native.vrhip_destroy(None) == 0
     assert native.vrhip_build_flat(None, None, None, None, 0, None, 0, 4, None, None, None, None, None, None,
                                    None) == -1
