@@ -7,7 +7,11 @@ camera, Fresnel 0.1/3.0.  One "step" = one progressive accumulation step of
 FRAMES_PER_STEP frames over the whole 1280x720 image (inputs resident in
 HBM), ending with the tile gather to rank 0 when N > 1.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F] [--config C2]
+
+--config C3 / C5 runs the same measurement on another BASELINE.json
+configuration (C3: HDRI + textured knot at 1280x720; C5: 1M-triangle knot
+under HDRI at 3840x2160); the default and the number of record is C2.
 
 N > 1: one process per GPU (torch.distributed.run), 16x16 pixel
 tiles dealt round-robin, each rank renders its tiles of every frame, then one
@@ -36,7 +40,15 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-CFG = "C2"
+WORKLOADS = {
+    "C2": ("C2: Cornell box + 10k-tri torus knot, diffuse, 1280x720, 2 spp/frame, 4 bounces",
+           "synthetic (procedural Cornell box + 10k-tri torus knot; SURVEY.md 8d C2)"),
+    "C3": ("C3: HDRI env + 10k-tri torus knot with diffuse/normal/specular maps + Fresnel, 1280x720, "
+           "2 spp/frame, 4 bounces",
+           "synthetic (procedural 2048x1024 HDRI, 1024^2 maps, 10k-tri torus knot; SURVEY.md 8d C3)"),
+    "C5": ("C5: 1M-tri torus knot (SBVH-depth tree) under HDRI, 3840x2160, 2 spp/frame, 4 bounces",
+           "synthetic (procedural 2048x1024 HDRI, 1M-tri torus knot; SURVEY.md 8d C5)"),
+}
 PROFILE_TRAFFIC = os.path.join(REPO, "profiles", "traffic_c2.json")
 
 
@@ -70,8 +82,8 @@ def cpu_baseline(scene: dict, budget_s: float, threads: int) -> dict:
     dt = time.perf_counter() - t0
     rows = paths // (2 * W)
     return {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ C restatement (glibc libm, -O2, OpenMP {threads} threads), C2 "
-                      f"1280x720, {rows} rows over {frames} frame(s) ({paths} paths, {dt:.1f} s)"}
+            "sample": f"oracle/ C restatement (glibc libm, -O2, OpenMP {threads} threads), {scene['name']} "
+                      f"{W}x{H}, {rows} rows over {frames} frame(s) ({paths} paths, {dt:.1f} s)"}
 
 
 def main():
@@ -80,6 +92,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames-per-step", type=int, default=16)
+    ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -108,6 +121,7 @@ def main():
     from vrenderer_pathtracer_amd import VRendererHIP, build_native, scenes
     from vrenderer_pathtracer_amd.tiles import TileGather, WHAT_RGBA8
     build_native()
+    CFG = args.config
     scene = scenes.make_scene(CFG)
     W, H = scene["width"], scene["height"]
     F = args.frames_per_step
@@ -178,7 +192,7 @@ def main():
         avg_launch_s = (kms / 1e3) / max(launches, 1)
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         traffic = None
-        if os.path.exists(PROFILE_TRAFFIC):
+        if CFG == "C2" and os.path.exists(PROFILE_TRAFFIC):   # rocprofv3 PMC of the C2 step
             try:
                 traffic = json.load(open(PROFILE_TRAFFIC)).get("hbm_bytes_per_launch")
             except Exception:
@@ -195,9 +209,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (procedural Cornell box + 10k-tri torus knot; SURVEY.md 8d C2)",
-            "config": {"workload": "C2: Cornell box + 10k-tri torus knot, diffuse, 1280x720, 2 spp/frame, "
-                                   "4 bounces", "width": W, "height": H, "frames_per_step": F,
+            "data": WORKLOADS[CFG][1],
+            "config": {"workload": WORKLOADS[CFG][0], "width": W, "height": H, "frames_per_step": F,
                        "paths_per_step": paths_per_step, "parallelism": f"tile{world}",
                        "gather": "RCCL gather of RGBA8 tiles to rank 0 per step" if world > 1 else "none"},
             "mrays_per_s": round(mrays, 3),
