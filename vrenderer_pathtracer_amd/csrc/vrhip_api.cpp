@@ -47,6 +47,12 @@ void dfree(T*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } }
 
 } // namespace
 
+// Path streams (see render_impl): launch i's kernels wait for the finish
+// pass of launch i - VR_PATH_STREAMS, the last reader of the same scratch.
+#ifndef VR_PATH_STREAMS
+#define VR_PATH_STREAMS 3
+#endif
+
 struct vrhip_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -77,9 +83,9 @@ struct vrhip_ctx {
     // path groups per pixel (0: automatic) and their result scratch
     uint32_t path_split = 0;
     uint32_t cu_count = 256;
-    // Render launches alternate between two path streams (parity 0/1), each
-    // with its own scratch, so a launch's paths can start while the previous
-    // launch drains; finish passes stay in order on `stream` (see render_impl)
+    // Render launches take the path streams in turn, each with its own
+    // scratch, so a launch's paths can start while the previous launch
+    // drains; finish passes stay in order on `stream` (see render_impl)
     struct Lane {
         hipStream_t s = nullptr;
         vr4* paths = nullptr;
@@ -90,7 +96,7 @@ struct vrhip_ctx {
         hipEvent_t done = nullptr;   // recorded on `s` after the render kernels
         hipEvent_t finished = nullptr;   // recorded on `stream` after the finish pass that read this scratch
         bool used = false;
-    } lane[2];
+    } lane[VR_PATH_STREAMS];
     uint32_t parity = 0;
     int overlap = -1;            // vrhip_set_overlap: 1 always, 0 never, -1 small launches only
     bool join = true;            // the next launches must wait for everything queued on `stream`
@@ -895,11 +901,13 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         p.n_frames = k;
         p.split = std::min<uint32_t>(split_max, 2u * k);
         for (uint32_t i = 0; i < k; ++i) p.times[i] = times ? times[done + i] : time_seed;
-        // Path launches run on the two path streams in turn: launch i's render
-        // kernels wait only for the finish pass of launch i-2 (the last reader
-        // of the same scratch), so they start while launch i-1 drains its
-        // longest paths; the finish passes run in order on `stream`.  The
-        // counting variant accumulates in place on `stream`.
+        // Path launches take the VR_PATH_STREAMS path streams in turn: launch
+        // i's render kernels wait only for the finish pass of launch i - 3
+        // (the last reader of the same scratch), so they start while launch
+        // i-1 drains its longest paths -- and are not held up by launch i-1's
+        // finish pass, which itself waits for CUs until that drain.  The
+        // finish passes run in order on `stream`.  The counting variant
+        // accumulates in place on `stream`.
         // Without overlap every launch uses the same path stream, so it waits
         // for the previous one (and its finish pass, below) like a single stream.
         const bool ovl = c->overlap > 0 || (c->overlap < 0 && (size_t)p.path_stride * 2u * k < ((size_t)1 << 24));
@@ -907,7 +915,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         auto& l = c->lane[c->parity];
         hipStream_t rs = p.use_scratch ? l.s : c->stream;
         if (p.use_scratch) {
-            if (ovl) c->parity ^= 1u;
+            if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = l.paths; p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
             if (l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
         }
