@@ -1145,6 +1145,12 @@ __global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_k
     }
 }
 
+// Kernels without the example sphere (whose hits need the u,v slots) store
+// the camera ray's direction in the primary record instead, so a path starts
+// without recomputing it (two f64 divisions and a normalisation).
+template <uint32_t FEAT>
+constexpr bool prim_has_dir() { return (FEAT & F_EXAMPLE) == 0; }
+
 // Primary hits, one thread per owned pixel: the camera ray's closest hit
 // (the HitRec intersect_scene returns: t, kind, idx, barycentrics,
 // example-sphere u,v), two float4s per pixel in the scratch order of
@@ -1170,10 +1176,14 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
     const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     Cnt cnt;
     HitRec hr;
-    (void)intersect_scene<STACK, false, FEAT>(p, camera_ray(p, x, y), hr, L, cnt);
+    const Ray cam = camera_ray(p, x, y);
+    (void)intersect_scene<STACK, false, FEAT>(p, cam, hr, L, cnt);
     vr4* dst = p.prim + 2u * ((size_t)tile * kBlockThreads + tid);
     dst[0] = mk4(hr.t, __int_as_float(hr.kind), __int_as_float(hr.idx), hr.bu);
-    dst[1] = mk4(hr.bv, hr.su, hr.sv, 0.f);
+    if constexpr (prim_has_dir<FEAT>())
+        dst[1] = mk4(hr.bv, cam.d.x, cam.d.y, cam.d.z);   // the paths reuse the camera ray too
+    else
+        dst[1] = mk4(hr.bv, hr.su, hr.sv, 0.f);
 }
 
 // Path-pool render (the default for mesh scenes), a persistent kernel over
@@ -1280,10 +1290,17 @@ __global__ void __launch_bounds__(wave_block(STACK), VR_MIN_WAVES_PER_SIMD) rend
         uint32_t s2 = y * p.times[f];
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
         path_begin(ps, s1, s2);
-        ray = camera_ray(p, x, y);
         const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
         hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
-        hr.bv = b.x; hr.su = b.y; hr.sv = b.z;
+        hr.bv = b.x;
+        if constexpr (prim_has_dir<FEAT>()) {
+            hr.su = hr.sv = 0.f;
+            ray.o = p.cam_o;
+            ray.d = mk4(b.y, b.z, b.w, (p.cam_d.w + p.cx.w) + p.cy.w);   // camera_ray's .w
+        } else {
+            hr.su = b.y; hr.sv = b.z;
+            ray = camera_ray(p, x, y);
+        }
         state = LS_SHADE;
     };
     start(cur_sub, cur_q, (uint32_t)lane);
