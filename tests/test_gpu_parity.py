@@ -271,6 +271,35 @@ def test_pipelined_steps_with_scene_changes_equal_synchronous(native, cfg, overl
     assert np.array_equal(c_sync, c_pipe)
 
 
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_more_frames_than_one_launch_bitexact(native, oracle, overlap):
+    """A render call of 70 frames is two launches (64 + 6); with overlap they
+    run on different path streams."""
+    sc = scenes.make_scene("C2", 32, 32)
+    times = [sc["time"] + i for i in range(70)]
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.set_overlap(overlap)
+    r.render(frames=70, times=times)
+    got = r.read_accum()
+    assert r.getFrameCount() == 70
+    r.cleanUp()
+    ref, _, _, _ = po.render(sc, frames=70, times=times, libm=po.LIBM_PORTABLE)
+    assert_bitexact(got, ref, sc, "accum")
+
+
+def test_single_tile_and_empty_rank(native, oracle):
+    """One 16x16 tile (4 chunks per path for 256 resident blocks) renders
+    correctly; a rank that owns no tile renders nothing and does not hang."""
+    sc = scenes.make_scene("C3", 16, 16)
+    times = [sc["time"], sc["time"] + 1]
+    a, _, _, _ = gpu_render(sc, 2, times)
+    ref, _, _, _ = po.render(sc, frames=2, times=times, libm=po.LIBM_PORTABLE)
+    assert_bitexact(a, ref, sc, "accum")
+    empty, _, _, nf = gpu_render(sc, 2, times, tiling=(1, 2))
+    assert nf == 2 and not empty.any()
+
+
 @pytest.mark.parametrize("cfg,w,h", [("C2", 96, 64), ("C3", 96, 64), ("C4", 96, 64)])
 def test_strict_counts_equal_oracle_counts(native, oracle, cfg, w, h):
     """Strict traversal visits exactly the nodes and tests exactly the
