@@ -523,7 +523,6 @@ __device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Tr
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
-    int* stk = L.stk;
     int leafAddr = 0;
     while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
         if (HAS(F_WIDE)) node_step4<COUNT, FEAT>(p, r, tr, L, cnt);
@@ -1053,8 +1052,10 @@ __device__ __forceinline__ Ray camera_ray(const RenderParams& p, uint32_t x, uin
 #ifndef VR_MIN_WAVES_PER_SIMD
 #define VR_MIN_WAVES_PER_SIMD 4
 #endif
+// 64-entry stacks take 64 KiB of LDS per 256 threads: at most 2 waves/SIMD
+constexpr int min_waves(int stack) { return stack > 32 ? 2 : VR_MIN_WAVES_PER_SIMD; }
 template <int STACK, bool COUNT, uint32_t FEAT>
-__global__ void __launch_bounds__(kBlockThreads, VR_MIN_WAVES_PER_SIMD) render_kernel(const RenderParams p)
+__global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel(const RenderParams p)
 {
     constexpr int CN = cache_nodes(STACK);
     __shared__ int lds_stack[STACK * kBlockThreads];
@@ -1225,7 +1226,7 @@ static_assert(VR_WAVE_BLOCK % kBlockThreads == 0, "VR_WAVE_BLOCK must be a multi
 constexpr int wave_block(int stack) { return stack <= 32 ? VR_WAVE_BLOCK : kBlockThreads; }
 
 template <int STACK, uint32_t FEAT>
-__global__ void __launch_bounds__(wave_block(STACK), VR_MIN_WAVES_PER_SIMD) render_wave_kernel(const RenderParams p)
+__global__ void __launch_bounds__(wave_block(STACK), min_waves(STACK)) render_wave_kernel(const RenderParams p)
 {
     constexpr int BT = wave_block(STACK);
     constexpr int CN = cache_nodes(STACK, 0, BT);
