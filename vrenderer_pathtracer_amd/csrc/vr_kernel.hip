@@ -1458,9 +1458,11 @@ template <int STACK, uint32_t FEAT>
 static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
     hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
-    // p.wave_blocks counts 256-thread blocks
+    // one resident set: min_waves(STACK) waves per SIMD, 4 SIMDs per CU
     constexpr int BT = wave_block(STACK);
-    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT>), dim3(p.wave_blocks / (BT / kBlockThreads)),
+    constexpr uint32_t per_cu = (4u * (uint32_t)min_waves(STACK)) / (uint32_t)(BT / 64) > 0u
+                                    ? (4u * (uint32_t)min_waves(STACK)) / (uint32_t)(BT / 64) : 1u;
+    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT>), dim3(p.wave_blocks * per_cu),
                        dim3(BT), 0, s, p);
 }
 

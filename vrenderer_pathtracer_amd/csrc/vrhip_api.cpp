@@ -883,9 +883,10 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
                 c->join = true;
             }
         }
-        // the path-pool kernel is persistent: one resident set of blocks
-        // (4 per CU at 4 waves/SIMD) draining a work queue
-        p.wave_blocks = c->cu_count * 4u;
+        // the path-pool kernel is persistent: one resident set of blocks per
+        // CU (the launcher sizes it from the kernel's occupancy) draining the
+        // work queues
+        p.wave_blocks = c->cu_count;
     }
     (void)hipGetLastError();            // launches below report their own errors only
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
