@@ -1225,6 +1225,10 @@ static_assert(VR_WAVE_BLOCK % kBlockThreads == 0, "VR_WAVE_BLOCK must be a multi
 // 64-entry stacks (trees deeper than 30) need 64 KB per 256 threads
 constexpr int wave_block(int stack) { return stack <= 32 ? VR_WAVE_BLOCK : kBlockThreads; }
 
+#ifndef VR_XCD_BANDS
+#define VR_XCD_BANDS 128
+#endif
+
 template <int STACK, uint32_t FEAT>
 __global__ void __launch_bounds__(wave_block(STACK), min_waves(STACK)) render_wave_kernel(const RenderParams p)
 {
@@ -1246,19 +1250,42 @@ __global__ void __launch_bounds__(wave_block(STACK), min_waves(STACK)) render_wa
     // out chunks j, j + Q, j + 2Q, ... (one device-scope atomic per chunk; a
     // single head saturates: MI355X_MICROARCH "dequeue").  A wave draws from
     // its block's queue and, once that is drained, from the following ones.
+    // With VR_XCD_BANDS (default 128 sub-tiles = 32 tiles) the sub-tiles are
+    // dealt to the 8 XCDs in bands, so each XCD's L2 serves a coherent part of
+    // the image (C2 +0.7 %, C3 +1.7 %, C5 +0.7 % over chunk-interleaved queues).
     constexpr uint32_t Q = VR_QUEUES;
+    static_assert(Q % 8u == 0u, "VR_QUEUES must be a multiple of the 8 XCDs");
     const uint32_t n_chunks = n_sub * n_paths;
+    (void)n_chunks;
     uint32_t qj = blockIdx.x % Q, drained = 0;
     auto grab = [&](uint32_t& sub, uint32_t& path) {       // wave-uniform; sub = ~0u when no work is left
         for (;;) {
             uint32_t v = 0;
             if (lane == 0) v = atomicAdd(p.chunk_ctr + qj * kQueueStride, 1u);
+#if VR_XCD_BANDS
+            // queue j serves XCD j % 8 (blocks b % 16 == j under round-robin
+            // dispatch): bands of VR_XCD_BANDS sub-tiles dealt round-robin to
+            // the XCDs, each XCD's chunks sub-major, alternated between its
+            // Q / 8 queues
+            const uint32_t x = qj % 8u, h = qj / 8u;
+            const uint32_t e = __builtin_amdgcn_readfirstlane(v) * (Q / 8u) + h;
+            const uint32_t per_band = (uint32_t)VR_XCD_BANDS * n_paths;
+            const uint32_t g = e / per_band, o = e - g * per_band;
+            const uint32_t r = o / n_paths;
+            const uint32_t sb = (g * 8u + x) * (uint32_t)VR_XCD_BANDS + r;
+            if (sb < n_sub) {
+                sub = sb;
+                path = o - r * n_paths;
+                return;
+            }
+#else
             const uint32_t c = __builtin_amdgcn_readfirstlane(v) * Q + qj;
             if (c < n_chunks) {
                 sub = c / n_paths;
                 path = c - sub * n_paths;
                 return;
             }
+#endif
             if (++drained == Q) { sub = ~0u; path = 0; return; }
             qj = qj + 1u == Q ? 0u : qj + 1u;
         }
