@@ -537,6 +537,8 @@ int vrhip_destroy(vrhip_ctx* c)
 int vrhip_set_stream(vrhip_ctx* c, void* s)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    // work queued on the old stream (finish passes) must not reorder with the new one
+    if (c->stream && hipSetDevice(c->device) == hipSuccess) (void)hipStreamSynchronize(c->stream);
     quiesce(c);
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return VRHIP_OK;
@@ -799,6 +801,37 @@ static uint32_t choose_split(const vrhip_ctx* c, uint32_t n_tiles, uint32_t k)
     return std::max<uint32_t>(1u, std::min<uint32_t>(t, 2u * k));
 }
 
+// Scratch of one path stream, allocated when the stream is first used and
+// grown when a launch needs more (growing waits for every reader first).
+static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t path_stride)
+{
+    const size_t prim_need = 2 * (size_t)path_stride;
+    if ((l.paths && need > l.paths_cap) || (l.prim && prim_need > l.prim_cap)) {
+        quiesce(c);                                       // the finish passes read the scratch too
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    if (need > l.paths_cap) {
+        dfree(l.paths);
+        l.paths_cap = 0;
+        HIP_TRY(hipMalloc((void**)&l.paths, need * sizeof(vr4)));
+        l.paths_cap = need;
+    }
+    if (prim_need > l.prim_cap) {
+        dfree(l.prim);
+        l.prim_cap = 0;
+        HIP_TRY(hipMalloc((void**)&l.prim, prim_need * sizeof(vr4)));
+        l.prim_cap = prim_need;
+    }
+    if (!l.chunk_ctr) {
+        const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * VR_QUEUES;
+        HIP_TRY(hipMalloc((void**)&l.chunk_ctr, bytes));
+        HIP_TRY(hipMemsetAsync(l.chunk_ctr, 0, bytes, c->stream));
+        HIP_TRY(hipEventRecord(c->ev_join, c->stream));
+        HIP_TRY(hipStreamWaitEvent(l.s, c->ev_join, 0));
+    }
+    return VRHIP_OK;
+}
+
 static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed, bool count)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
@@ -857,32 +890,8 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     const uint32_t split_max = count ? 1u : choose_split(c, n_tiles, k_max);
     p.path_stride = n_tiles * (uint32_t)vr::kBlockThreads;
     p.use_scratch = count ? 0u : 1u;   // the counting variant accumulates in place
+    const size_t need = (size_t)2 * k_max * p.path_stride;   // scratch float4s of the largest launch
     if (p.use_scratch) {
-        const size_t need = (size_t)2 * k_max * p.path_stride;
-        for (auto& l : c->lane) {
-            if (need > l.paths_cap || 2 * (size_t)p.path_stride > l.prim_cap) {
-                quiesce(c);                               // the finish passes read the scratch too
-                HIP_TRY(hipStreamSynchronize(c->stream));
-            }
-            if (need > l.paths_cap) {
-                dfree(l.paths);
-                l.paths_cap = 0;
-                HIP_TRY(hipMalloc((void**)&l.paths, need * sizeof(vr4)));
-                l.paths_cap = need;
-            }
-            if (2 * (size_t)p.path_stride > l.prim_cap) {
-                dfree(l.prim);
-                l.prim_cap = 0;
-                HIP_TRY(hipMalloc((void**)&l.prim, 2 * (size_t)p.path_stride * sizeof(vr4)));
-                l.prim_cap = 2 * (size_t)p.path_stride;
-            }
-            if (!l.chunk_ctr) {
-                const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * VR_QUEUES;
-                HIP_TRY(hipMalloc((void**)&l.chunk_ctr, bytes));
-                HIP_TRY(hipMemsetAsync(l.chunk_ctr, 0, bytes, c->stream));
-                c->join = true;
-            }
-        }
         // the path-pool kernel is persistent: one resident set of blocks per
         // CU (the launcher sizes it from the kernel's occupancy) draining the
         // work queues
@@ -916,6 +925,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         auto& l = c->lane[c->parity];
         hipStream_t rs = p.use_scratch ? l.s : c->stream;
         if (p.use_scratch) {
+            if ((rc = ensure_lane(c, l, need, p.path_stride)) != VRHIP_OK) return rc;
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = l.paths; p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
             if (l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
