@@ -1473,12 +1473,19 @@ __global__ void selftest_math_kernel(int fn, const float* a, const float* b, flo
 // ---- host launchers --------------------------------------------------------
 // Feature specialisations, smallest first (BASELINE configs C1..C5); the
 // generic kernel covers everything else, deep trees and the counting variant.
+// the 4-wide traversal is compiled in only with -DVR_BVH4 (the host sets the
+// runtime flag only then)
+#ifdef VR_BVH4
+constexpr uint32_t kWide = F_WIDE;
+#else
+constexpr uint32_t kWide = 0u;
+#endif
 constexpr uint32_t kFeatAll =
-    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT | F_WIDE;
-constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH | F_WIDE;                          // C2, Cornell-only
+    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT | kWide;
+constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH | kWide;                          // C2, Cornell-only
 constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                              // C1
-constexpr uint32_t kFeatHdriMesh = F_MESH | F_WIDE;                                         // C5
-constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_WIDE; // C3
+constexpr uint32_t kFeatHdriMesh = F_MESH | kWide;                                         // C5
+constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | kWide; // C3
 constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
 
 template <int STACK, uint32_t FEAT>
