@@ -35,7 +35,11 @@ namespace vr {
 // Scene features are tested twice: against the kernel's compile-time feature
 // set FEAT (code for absent features is compiled out, cutting VGPRs) and
 // against the launch's runtime flags.
-#define HAS(F) ((FEAT & (F)) != 0 && (p.flags & (F)) != 0)
+// Feature test inside a kernel specialised on FEAT.  Specialisations marked
+// F_EXACT are launched only when the scene's flags equal their feature set,
+// so their tests fold at compile time; the generic kernel tests the flags.
+constexpr uint32_t F_EXACT = 1u << 31;
+#define HAS(F) ((FEAT & (F)) != 0 && ((FEAT & F_EXACT) != 0 || (p.flags & (F)) != 0))
 
 // ---- float4 with the reference's operator semantics (MathHelpers.cuh:85-196)
 __device__ __forceinline__ vr4 mk4(float x, float y, float z, float w) { vr4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
@@ -1474,7 +1478,7 @@ __global__ void selftest_math_kernel(int fn, const float* a, const float* b, flo
 // Feature specialisations, smallest first (BASELINE configs C1..C5); the
 // generic kernel covers everything else, deep trees and the counting variant.
 // the 4-wide traversal is compiled in only with -DVR_BVH4 (the host sets the
-// runtime flag only then)
+// runtime flag only then; such launches take the generic kernel)
 #ifdef VR_BVH4
 constexpr uint32_t kWide = F_WIDE;
 #else
@@ -1482,10 +1486,10 @@ constexpr uint32_t kWide = 0u;
 #endif
 constexpr uint32_t kFeatAll =
     F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT | kWide;
-constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH | kWide;                          // C2, Cornell-only
+constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH;                                  // C2
 constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                              // C1
-constexpr uint32_t kFeatHdriMesh = F_MESH | kWide;                                         // C5
-constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | kWide; // C3
+constexpr uint32_t kFeatHdriMesh = F_MESH;                                                 // C5
+constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;        // C3
 constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
 
 template <int STACK, uint32_t FEAT>
@@ -1527,7 +1531,6 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool
     if (n_tiles == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     const uint32_t need = p.flags & kFeatAll;
-    auto covers = [need](uint32_t feat) { return (need & ~feat) == 0u; };
     const uint32_t blocks = n_tiles * p.split;   // split == 1 for the counting variant
     if (count || stack_depth > 32) {
         if (count) {
@@ -1536,16 +1539,16 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool
         } else {
             launch_wave<64, kFeatAll>(p, n_tiles, s);
         }
-    } else if (covers(kFeatCornellMesh)) {
-        launch_spec<kFeatCornellMesh>(p, n_tiles, stack_depth, s);
-    } else if (covers(kFeatCornellSphere)) {
-        launch_spec<kFeatCornellSphere>(p, n_tiles, stack_depth, s);
-    } else if (covers(kFeatHdriMesh)) {
-        launch_spec<kFeatHdriMesh>(p, n_tiles, stack_depth, s);
-    } else if (covers(kFeatHdriMeshTex)) {
-        launch_spec<kFeatHdriMeshTex>(p, n_tiles, stack_depth, s);
-    } else if (covers(kFeatHdriBrdfSphere)) {
-        launch_spec<kFeatHdriBrdfSphere>(p, n_tiles, stack_depth, s);
+    } else if (need == kFeatCornellMesh) {
+        launch_spec<kFeatCornellMesh | F_EXACT>(p, n_tiles, stack_depth, s);
+    } else if (need == kFeatCornellSphere) {
+        launch_spec<kFeatCornellSphere | F_EXACT>(p, n_tiles, stack_depth, s);
+    } else if (need == kFeatHdriMesh) {
+        launch_spec<kFeatHdriMesh | F_EXACT>(p, n_tiles, stack_depth, s);
+    } else if (need == kFeatHdriMeshTex) {
+        launch_spec<kFeatHdriMeshTex | F_EXACT>(p, n_tiles, stack_depth, s);
+    } else if (need == kFeatHdriBrdfSphere) {
+        launch_spec<kFeatHdriBrdfSphere | F_EXACT>(p, n_tiles, stack_depth, s);
     } else {
         launch_spec<kFeatAll>(p, n_tiles, stack_depth, s);
     }
