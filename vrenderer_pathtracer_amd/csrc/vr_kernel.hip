@@ -468,7 +468,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, 
 // the closest-hit update (:379-386).  Evaluated branch-free: every early
 // return of the reference becomes a term of the final predicate (the values
 // computed for a surviving triangle are the same operations in the same order).
-struct TriV { vr3 a0, a1, a2; };
+struct TriV { vr3 a0, a1, a2; };        // v0, e1 = v1 - v0, e2 = v2 - v0 (p.tri_e)
 template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, Trav& tr, int k, const TriV& t, Cnt& cnt)
 {
@@ -476,9 +476,8 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
     if (COUNT) cnt.tris++;
     VR_LANE(2, 3);
     const vr4 v0 = mk4(t.a0.x, t.a0.y, t.a0.z, 0.f);
-    const vr4 v1 = mk4(t.a1.x, t.a1.y, t.a1.z, 0.f);
-    const vr4 v2 = mk4(t.a2.x, t.a2.y, t.a2.z, 0.f);
-    const vr4 e1 = sub4(v1, v0), e2 = sub4(v2, v0);
+    const vr4 e1 = mk4(t.a1.x, t.a1.y, t.a1.z, 0.f);         // v1 - v0, v2 - v0 (RayIntersection.cuh:62-63), from the upload
+    const vr4 e2 = mk4(t.a2.x, t.a2.y, t.a2.z, 0.f);
     const vr4 pv = cross4(r.d, e2);
     const float det = dot4(e1, pv);
     const float inv_det = 1.f / det;
@@ -498,9 +497,9 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 __device__ __forceinline__ TriV tri_load(const RenderParams& p, int k)
 {
 #ifdef VR_DROP_TRIS
-    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, 0u);     // timing probe: loads return 0
+    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, 0u);     // timing probe: loads return 0
 #else
-    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.verts, p.n_tris * 36u);
+    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, p.n_tris * 36u);
 #endif
     const int toff = k * 36;
     TriV t;

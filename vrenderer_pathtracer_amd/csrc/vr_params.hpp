@@ -57,7 +57,8 @@ struct RenderParams {
     uint32_t n_nodes4;
     const vr4* bvh16;                // same nodes, conservative fp16 boxes, 32 B each (culled traversal)
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
-    const vr3* verts;                // 3 vertices per triangle, compact leaf order
+    const vr3* verts;                // 3 vertices per triangle, compact leaf order (face normal at shading)
+    const vr3* tri_e;                // per triangle (v0, v1 - v0, v2 - v0): the traversal's copy
     uint32_t n_tris;                 // triangles in verts/normals/tangents/uvs
     const vr4* normals;
     const vr4* tangents;

@@ -70,7 +70,7 @@ struct vrhip_ctx {
     bool cornell = false, example = false, view_brdf = false;
     bool strict = false;          // exact reference traversal (no t-culling)
     // mesh
-    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr4* bvh4 = nullptr; vr3* verts = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
+    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr4* bvh4 = nullptr; vr3* verts = nullptr; vr3* tri_e = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
     uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0, dev_nodes4 = 0;
     bool mesh = false;
@@ -155,6 +155,7 @@ struct DeviceMesh {
     std::vector<vr4> nodes16;        // 2 x 16 B per node: conservative fp16 boxes + child indices
     std::vector<vr4> nodes4;         // 4-wide nodes, 7 x 16 B each (collapsed binary tree)
     std::vector<vr3> tris;           // packed 12 B vertices (vertex .w never reaches a result)
+    std::vector<vr3> tri_e;          // per triangle v0, v1 - v0, v2 - v0 (fp32, the kernel's own subtractions)
     std::vector<vr2> uvs;
 };
 
@@ -422,6 +423,17 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
         dm.tangents = dm.normals;
         dm.uvs.push_back(vr2{ 0, 0 });
     }
+    // The Moller-Trumbore edges are the same fp32 subtractions whichever side
+    // performs them; precomputed, the triangle test reads v0 and both edges
+    // and skips 6 VALU ops per test.  The face normal at shading keeps using
+    // the vertices (v0 - v1 is not -(v1 - v0) for signed zeros).
+    dm.tri_e.resize(dm.tris.size());
+    for (size_t t = 0; t + 2 < dm.tris.size(); t += 3) {
+        const vr3 a = dm.tris[t], b = dm.tris[t + 1], d = dm.tris[t + 2];
+        dm.tri_e[t] = a;
+        dm.tri_e[t + 1] = vr3{ b.x - a.x, b.y - a.y, b.z - a.z };
+        dm.tri_e[t + 2] = vr3{ d.x - a.x, d.y - a.y, d.z - a.z };
+    }
     return true;
 }
 
@@ -513,7 +525,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     quiesce(c);
     dfree(c->accum); dfree(c->rgba); dfree(c->depth);
-    dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->verts); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
+    dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->verts); dfree(c->tri_e); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     for (int i = 0; i < 2; ++i)
         if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
@@ -596,6 +608,7 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     if ((rc = upload(c, c->bvh4, dm.nodes4.data(), dm.nodes4.size() * 16))) return rc;
     c->dev_nodes4 = (uint32_t)(dm.nodes4.size() / 7);
     if ((rc = upload(c, c->verts, dm.tris.data(), nt * sizeof(vr3)))) return rc;
+    if ((rc = upload(c, c->tri_e, dm.tri_e.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->normals, dm.normals.data(), nt * 16))) return rc;
     if ((rc = upload(c, c->tangents, dm.tangents.data(), nt * 16))) return rc;
     if ((rc = upload(c, c->uvs, dm.uvs.data(), nt * 8))) return rc;
@@ -867,7 +880,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.tiles_x = p.wr / 16u;
     p.rank = c->rank; p.nranks = c->nranks;
     p.bvh4 = c->bvh4; p.n_nodes4 = c->mesh ? c->dev_nodes4 : 0;
-    p.bvh = c->bvh; p.bvh16 = c->bvh16; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
+    p.bvh = c->bvh; p.bvh16 = c->bvh16; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.tri_e = c->tri_e; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
     p.hdr = c->hdr; p.hdr_w = c->hdr_w; p.hdr_h = c->hdr_h;
     for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
     p.brdf = c->brdf;
