@@ -301,6 +301,26 @@ def test_random_soup_bitexact_vs_portable_oracle(native, oracle, cfg, leaf):
     assert diff.mean() <= 1e-3, int(diff.sum())
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_stack24_tree_bitexact_vs_portable_oracle(native, oracle, cfg):
+    """The torus knot with one triangle per leaf is 16 levels deep, so the
+    launches take the 24-entry-stack kernels (trees of depth 16-23, C5's
+    class): strict bit-exact against the oracle, culled equal to strict."""
+    from vrenderer_pathtracer_amd import build_flat, validate_flat
+    sc = scenes.make_scene(cfg, 96, 64)
+    sc["mesh_flat"] = build_flat(scenes.torus_knot(100, 50), max_leaf_tris=1)
+    depth, _ = validate_flat(sc["mesh_flat"])
+    assert 15 < depth <= 23, depth
+    times = [sc["time"], sc["time"] + 1]
+    oa, orgba, _, _ = po.render(sc, frames=2, times=times, libm=po.LIBM_PORTABLE)
+    sa, srgba, _, _ = gpu_render(sc, 2, times, strict=True)
+    assert_bitexact(sa, oa, sc, "accum (strict)")
+    assert_bitexact(srgba, orgba, sc, "rgba8 (strict)")
+    ca, _, _, _ = gpu_render(sc, 2, times)
+    diff = (rendered(ca, sc).view(np.uint32) != rendered(sa, sc).view(np.uint32)).any(-1)
+    assert diff.mean() <= 1e-3, int(diff.sum())
+
+
 @pytest.mark.parametrize("overlap", [1, 0])
 def test_more_frames_than_one_launch_bitexact(native, oracle, overlap):
     """A render call of 70 frames is two launches (64 + 6); with overlap they

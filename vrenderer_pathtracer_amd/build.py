@@ -20,8 +20,13 @@ ARCH = os.environ.get("VRHIP_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: results are defined without FMA contraction (parity
 # with the CPU oracle); division and sqrt stay IEEE (hipcc default).
+# -packed-fp32-ops: no v_pk_{add,mul,fma}_f32.  The path kernel's float math
+# comes in 3-component vectors, and pairing it costs more v_mov_b32 operand
+# shuffles (and registers: C2 path kernel 111 -> 89 VGPRs) than the packed
+# ops save; the kernel is VALU-issue heavy, so C2 +10 %, C3 +2.7 %, C5 +0.9 %
+# (identical results: packed and scalar f32 ops round the same).
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", "-pthread",
-               f"--offload-arch={ARCH}"]
+               f"--offload-arch={ARCH}", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
 def _hipcc() -> str:

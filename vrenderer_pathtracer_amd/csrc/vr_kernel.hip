@@ -1221,22 +1221,40 @@ enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3 };
 // Block size of the path kernel: its blocks hold no tiles, so one block of
 // 1,024 threads per CU shares one LDS node cache four times the size of a
 // 256-thread block's (at the same 4 waves/SIMD).
-#ifndef VR_WAVE_BLOCK
-#define VR_WAVE_BLOCK 1024
+// Path-kernel residency by stack size: with 16- and 24-entry stacks (C2, C3;
+// C5) VR_PATH_WAVES waves per SIMD in VR_PATH_BLOCK-thread blocks; 32-entry
+// stacks 4 waves in one 1,024-thread block per CU (the stacks alone take
+// 128 KB); 64-entry stacks 2 waves in 256-thread blocks.  Measured (C2 / C3,
+// no packed f32): 4 waves in 1,024 threads 3,029 / 10,724; 5 in 256: 2,956 /
+// 10,503; 6 in 256: 3,228 / 11,352; 6 in 512: 2,952 / 10,483; 6 in 768:
+// 3,406 / 12,193; 7 in 256 (spills): 3,317 / 11,290.
+#ifndef VR_PATH_WAVES
+#define VR_PATH_WAVES 6
 #endif
-static_assert(VR_WAVE_BLOCK % kBlockThreads == 0, "VR_WAVE_BLOCK must be a multiple of 256");
-// 64-entry stacks (trees deeper than 30) need 64 KB per 256 threads
-constexpr int wave_block(int stack) { return stack <= 32 ? VR_WAVE_BLOCK : kBlockThreads; }
+#ifndef VR_PATH_BLOCK
+#define VR_PATH_BLOCK 768
+#endif
+static_assert(VR_PATH_BLOCK % kBlockThreads == 0, "VR_PATH_BLOCK must be a multiple of 256");
+static_assert((4 * VR_PATH_WAVES * 64) % VR_PATH_BLOCK == 0, "whole blocks per CU");
+constexpr int wave_block(int stack) { return stack <= 24 ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads; }
+constexpr int path_waves(int stack) { return stack <= 24 ? VR_PATH_WAVES : stack <= 32 ? 4 : 2; }
+constexpr int path_blocks_per_cu(int stack) { return 4 * path_waves(stack) * 64 / wave_block(stack); }
+// LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
+// the node cache takes what the stacks leave (56 B per node)
+constexpr int path_cache_nodes(int stack) {
+    return (163840 / path_blocks_per_cu(stack) - wave_block(stack) - stack * wave_block(stack) * 4) / 56 > 0
+               ? (163840 / path_blocks_per_cu(stack) - wave_block(stack) - stack * wave_block(stack) * 4) / 56 : 1;
+}
 
 #ifndef VR_XCD_BANDS
 #define VR_XCD_BANDS 128
 #endif
 
 template <int STACK, uint32_t FEAT>
-__global__ void __launch_bounds__(wave_block(STACK), min_waves(STACK)) render_wave_kernel(const RenderParams p)
+__global__ void __launch_bounds__(wave_block(STACK), path_waves(STACK)) render_wave_kernel(const RenderParams p)
 {
     constexpr int BT = wave_block(STACK);
-    constexpr int CN = cache_nodes(STACK, 0, BT);
+    constexpr int CN = path_cache_nodes(STACK);
     __shared__ int lds_stack[STACK * BT];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
@@ -1495,10 +1513,9 @@ template <int STACK, uint32_t FEAT>
 static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
     hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
-    // one resident set: min_waves(STACK) waves per SIMD, 4 SIMDs per CU
+    // one resident set: path_waves(STACK) waves per SIMD, 4 SIMDs per CU
     constexpr int BT = wave_block(STACK);
-    constexpr uint32_t per_cu = (4u * (uint32_t)min_waves(STACK)) / (uint32_t)(BT / 64) > 0u
-                                    ? (4u * (uint32_t)min_waves(STACK)) / (uint32_t)(BT / 64) : 1u;
+    constexpr uint32_t per_cu = (uint32_t)path_blocks_per_cu(STACK);
     hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT>), dim3(p.wave_blocks * per_cu),
                        dim3(BT), 0, s, p);
 }
@@ -1521,6 +1538,8 @@ static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth
         hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
     else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
         launch_wave<16, FEAT>(p, n_tiles, s);
+    else if (stack_depth <= 24 && VR_MIN_SPEC_STACK <= 24)
+        launch_wave<24, FEAT>(p, n_tiles, s);
     else
         launch_wave<32, FEAT>(p, n_tiles, s);
 }

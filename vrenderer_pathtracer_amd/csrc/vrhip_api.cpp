@@ -888,7 +888,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     const uint32_t n_tiles = owned_tiles_of(c->W, c->H, c->rank, c->nranks);
     // stack entries needed: binary walk depth + 1; 4-wide walk 3 per 4-level + 1
     const int stack = (f & vr::F_WIDE) ? (c->bvh_depth <= 15 ? 32 : 64)
-                                       : (c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 30 ? 32 : 64);
+                                       : (c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 23 ? 24 : c->bvh_depth <= 30 ? 32 : 64);
     if (count) {
         if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
