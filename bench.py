@@ -221,9 +221,9 @@ def main():
                          "kernel": "primary_kernel+render_wave_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                          "launches": launches,
                          "note": "algorithmic bytes of the reference algorithm (SURVEY 8d), served mostly from "
-                                 "L2/LDS (traffic = physical HBM bytes per launch); consecutive launches overlap on "
-                                 "two path streams, so avg_launch_ms includes time shared with the neighbouring "
-                                 "launch"},
+                                 "L2/LDS (traffic = physical HBM bytes per launch); launches of fewer than 2^24 paths "
+                                 "(sharded frames) overlap on three path streams, and then avg_launch_ms includes "
+                                 "time shared with the neighbouring launch"},
         }
         if not args.no_cpu and world == 1:
             threads = min(16, os.cpu_count() or 1)
