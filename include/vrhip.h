@@ -232,6 +232,11 @@ int vrhip_bvh_info(vrhip_ctx *ctx, uint32_t *depth, uint32_t *n_nodes, uint32_t 
 /* Evaluate the device libm on n inputs (test hook: 0 sin, 1 cos, 2 acos,
  * 3 atan2, 4 pow, 5 fmin, 6 fmax, 7 f2i); a,b,out host arrays of n floats. */
 int vrhip_selftest_math(int device, int fn, const float *a, const float *b, float *out, size_t n);
+/* Compare the kernels' reciprocal (rcp_rn: v_rcp_f32 + one Newton step, used
+ * for 1/det in the triangle test) with IEEE 1/x for every float bit pattern in
+ * [lo_bits, hi_bits) and its negation (test hook; hi_bits <= 2^31).
+ * *mismatches = count, *first_bad = smallest mismatching pattern or ~0u. */
+int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t *mismatches, uint32_t *first_bad);
 
 /* ---- host-side helpers (no device needed) ----------------------------- */
 /* Native BVH build + reference flattening (src/vRendererCuda.cpp:204-279)

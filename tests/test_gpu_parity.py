@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import pyoracle as po
-from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math
+from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math, selftest_rcp
 
 pytestmark = pytest.mark.gpu
 
@@ -95,6 +95,17 @@ def test_device_f2i_semantics(native):
     a = np.array([np.nan, 3e9, -3e9, 2.9, -2.9, 0.0], np.float32)
     got = selftest_math(7, a).view(np.int32)
     assert got.tolist() == [0, 2147483647, -2147483648, 2, -2, 0]
+
+
+def test_rcp_exhaustive(native):
+    # the triangle test's 1/det (rcp_rn, vr_math.hpp) equals IEEE 1.f/det for
+    # every float of magnitude in [2^-32, 2^125], both signs (2.6e9 inputs);
+    # only |det| >= VR_EPS (3e-10 > 2^-32) can accept a hit, larger |det|
+    # takes the division
+    lo = int(np.float32(2.0 ** -32).view(np.uint32))
+    hi = int(np.float32(2.0 ** 125).view(np.uint32)) + 1
+    n, first = selftest_rcp(lo, hi)
+    assert n == 0, f"{n} mismatches, first {first:#010x}"
 
 
 @pytest.mark.parametrize("cfg,w,h,frames", [

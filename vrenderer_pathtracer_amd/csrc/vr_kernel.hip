@@ -480,7 +480,16 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
     const vr4 e2 = mk4(t.a2.x, t.a2.y, t.a2.z, 0.f);
     const vr4 pv = cross4(r.d, e2);
     const float det = dot4(e1, pv);
+#ifndef VR_IEEE_DIV
+    // 1/det (RayIntersection.cuh:75): only lanes with |det| >= VR_EPS (> 2^-32) can accept the
+    // hit, and there rcp_rn is the IEEE quotient up to |det| = 2^125; a wave
+    // holding a larger (or non-finite) det takes the division
+    float inv_det;
+    if (__builtin_expect(__ballot(!(__builtin_fabsf(det) <= kRcpRnHi)) != 0ull, 0)) inv_det = 1.f / det;
+    else inv_det = rcp_rn(det);
+#else
     const float inv_det = 1.f / det;
+#endif
     const vr4 tv = sub4(r.o, v0);
     const float u = dot4(tv, pv) * inv_det;
     const vr4 q = cross4(tv, e1);
@@ -1594,6 +1603,37 @@ int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t 
     if (n_owned == 0) return 0;
     hipLaunchKernelGGL(pack_tiles_kernel, dim3(n_owned), dim3(256), 0, (hipStream_t)stream,
                        (const uint32_t*)src, (uint32_t*)dst, elem_bytes / 4u, W, tiles_x, rank, nranks, unpack);
+    return (int)hipGetLastError();
+}
+
+// Exhaustive check of rcp_rn against IEEE division over the float bit
+// patterns [lo, hi) of both signs: counts mismatches, records the smallest
+// mismatching pattern.
+__global__ void selftest_rcp_kernel(uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad)
+{
+    const uint32_t stride = gridDim.x * blockDim.x;        // hi <= 2^31: b + stride cannot wrap
+    unsigned long long bad = 0;
+    uint32_t first = 0xffffffffu;
+    for (uint32_t b = lo + blockIdx.x * blockDim.x + threadIdx.x; b < hi; b += stride) {
+#pragma unroll
+        for (int neg = 0; neg < 2; ++neg) {
+            const uint32_t bits = neg ? (b | 0x80000000u) : b;
+            const float x = __uint_as_float(bits);
+            if (__float_as_uint(rcp_rn(x)) != __float_as_uint(1.f / x)) {
+                ++bad;
+                first = bits < first ? bits : first;
+            }
+        }
+    }
+    if (bad) {
+        atomicAdd(n_bad, bad);
+        atomicMin(first_bad, first);
+    }
+}
+
+int launch_selftest_rcp(uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad, void* stream)
+{
+    hipLaunchKernelGGL(selftest_rcp_kernel, dim3(4096), dim3(256), 0, (hipStream_t)stream, lo, hi, n_bad, first_bad);
     return (int)hipGetLastError();
 }
 

@@ -256,6 +256,19 @@ __device__ __forceinline__ float pow_p(float x, float y)
     return sign * (float)r;
 }
 
+// 1/x rounded to nearest from the hardware reciprocal (v_rcp_f32, 1 ulp) and
+// one Newton step on the fma residual: 3 VALU ops instead of the 11 of the
+// IEEE division sequence.  Equal to 1.f / x (IEEE) for every |x| in
+// [2^-32, 2^125], shown on gfx950 by exhaustive comparison
+// (vrhip_selftest_rcp, tests/test_gpu_parity.py::test_rcp_exhaustive).
+__device__ __forceinline__ float rcp_rn(float x)
+{
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+constexpr float kRcpRnHi = 0x1p125f;
+
 // float -> int with CUDA cvt.rzi.s32.f32 semantics (truncate, saturate, NaN -> 0)
 __device__ __forceinline__ int f2i(float f)
 {

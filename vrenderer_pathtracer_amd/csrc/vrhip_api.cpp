@@ -1170,6 +1170,27 @@ int vrhip_selftest_math(int device, int fn, const float* a, const float* b, floa
     return VRHIP_OK;
 }
 
+int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches, uint32_t* first_bad)
+{
+    if (!mismatches || !first_bad) return fail(VRHIP_ERR_INVALID, "null argument");
+    if (lo_bits > hi_bits || hi_bits > 0x80000000u) return fail(VRHIP_ERR_INVALID, "bit range outside [0, 2^31]");
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, 16));
+    uint32_t* df = (uint32_t*)(d + 1);
+    const uint32_t init_first = 0xffffffffu;
+    HIP_TRY(hipMemset(d, 0, 8));
+    HIP_TRY(hipMemcpy(df, &init_first, 4, hipMemcpyHostToDevice));
+    int e = vr::launch_selftest_rcp(lo_bits, hi_bits, d, df, nullptr);
+    if (e) { (void)hipFree(d); return fail(VRHIP_ERR_HIP, "selftest launch failed"); }
+    unsigned long long n = 0;
+    HIP_TRY(hipMemcpy(&n, d, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    *mismatches = n;
+    return VRHIP_OK;
+}
+
 int vrhip_build_flat(const float* positions, const float* normals, const float* tangents, const float* uvs,
                      uint32_t n_verts, const uint32_t* tris, uint32_t n_tris, uint32_t max_leaf_tris,
                      float* bvh_out, size_t* n_bvh_f4, float* verts_out, float* normals_out,

@@ -387,6 +387,16 @@ def selftest_math(fn: int, a, b=None, device: int = 0) -> np.ndarray:
     return out
 
 
+def selftest_rcp(lo_bits: int, hi_bits: int, device: int = 0):
+    """Exhaustively compare the kernels' reciprocal with IEEE 1/x over the float
+    bit patterns [lo_bits, hi_bits) and their negations: (mismatches, first_bad)."""
+    n = ctypes.c_uint64(0)
+    first = ctypes.c_uint32(0)
+    check(_native.lib().vrhip_selftest_rcp(device, lo_bits, hi_bits, ctypes.byref(n), ctypes.byref(first)),
+          "vrhip_selftest_rcp")
+    return int(n.value), int(first.value)
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     rc = _native.lib().vrhip_device_count(ctypes.byref(n))
