@@ -332,6 +332,24 @@ def test_stack24_tree_bitexact_vs_portable_oracle(native, oracle, cfg):
     assert diff.mean() <= 1e-3, int(diff.sum())
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_large_and_small_launch_blocks_agree(native, cfg):
+    """A 10-frame 1280x720 launch (18.4 M paths) runs the path kernel in
+    768-thread blocks, one frame per call (1.8 M paths) in 256-thread
+    blocks: the accumulations are identical bit for bit."""
+    sc = scenes.make_scene(cfg)
+    times = [sc["time"] + i for i in range(10)]
+    big, _, _, n_big = gpu_render(sc, 10, times)
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    for t in times:
+        r.render(frames=1, times=[t])
+    small, n_small = r.read_accum(), r.getFrameCount()
+    r.cleanUp()
+    assert n_big == n_small
+    assert np.array_equal(big.view(np.uint32), small.view(np.uint32))
+
+
 @pytest.mark.parametrize("overlap", [1, 0])
 def test_more_frames_than_one_launch_bitexact(native, oracle, overlap):
     """A render call of 70 frames is two launches (64 + 6); with overlap they

@@ -1246,24 +1246,29 @@ enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3 };
 static_assert(VR_PATH_BLOCK % kBlockThreads == 0, "VR_PATH_BLOCK must be a multiple of 256");
 static_assert((4 * VR_PATH_WAVES * 64) % VR_PATH_BLOCK == 0, "whole blocks per CU");
 constexpr int wave_block(int stack) { return stack <= 24 ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads; }
+// Launches of fewer than 2^24 paths (sharded frames, RenderParams::small_blocks)
+// take 256-thread blocks at the same residency: a block frees its CU slot once
+// its 4 waves are done rather than 12, so the launch's drain overlaps the next
+// launch sooner.  Projected 8-rank C2 step 1.283 -> 1.193 ms (C3 0.468 ->
+// 0.420 ms), while whole frames keep the 768-thread blocks (C2 3,437 vs 3,244).
+constexpr int wave_block_small(int stack) { return stack <= 24 ? kBlockThreads : wave_block(stack); }
 constexpr int path_waves(int stack) { return stack <= 24 ? VR_PATH_WAVES : stack <= 32 ? 4 : 2; }
-constexpr int path_blocks_per_cu(int stack) { return 4 * path_waves(stack) * 64 / wave_block(stack); }
+constexpr int path_blocks_per_cu(int stack, int bt) { return 4 * path_waves(stack) * 64 / bt; }
 // LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
 // the node cache takes what the stacks leave (56 B per node)
-constexpr int path_cache_nodes(int stack) {
-    return (163840 / path_blocks_per_cu(stack) - wave_block(stack) - stack * wave_block(stack) * 4) / 56 > 0
-               ? (163840 / path_blocks_per_cu(stack) - wave_block(stack) - stack * wave_block(stack) * 4) / 56 : 1;
+constexpr int path_cache_nodes(int stack, int bt) {
+    return (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * 4) / 56 > 0
+               ? (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * 4) / 56 : 1;
 }
 
 #ifndef VR_XCD_BANDS
 #define VR_XCD_BANDS 128
 #endif
 
-template <int STACK, uint32_t FEAT>
-__global__ void __launch_bounds__(wave_block(STACK), path_waves(STACK)) render_wave_kernel(const RenderParams p)
+template <int STACK, uint32_t FEAT, int BT>
+__global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(const RenderParams p)
 {
-    constexpr int BT = wave_block(STACK);
-    constexpr int CN = path_cache_nodes(STACK);
+    constexpr int CN = path_cache_nodes(STACK, BT);
     __shared__ int lds_stack[STACK * BT];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
@@ -1523,9 +1528,14 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
     hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
     // one resident set: path_waves(STACK) waves per SIMD, 4 SIMDs per CU
-    constexpr int BT = wave_block(STACK);
-    constexpr uint32_t per_cu = (uint32_t)path_blocks_per_cu(STACK);
-    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT>), dim3(p.wave_blocks * per_cu),
+    constexpr int BT = wave_block(STACK), BTS = wave_block_small(STACK);
+    if (BTS != BT && p.small_blocks) {
+        hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * path_blocks_per_cu(STACK, BTS)),
+                           dim3(BTS), 0, s, p);
+        return;
+    }
+    constexpr uint32_t per_cu = (uint32_t)path_blocks_per_cu(STACK, BT);
+    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BT>), dim3(p.wave_blocks * per_cu),
                        dim3(BT), 0, s, p);
 }
 

@@ -52,6 +52,7 @@ struct RenderParams {
     vr4* prim;                       // per owned pixel: the camera ray's closest hit (2 x vr4, primary_kernel)
     uint32_t* chunk_ctr;             // render_wave_kernel's work queue heads (zeroed by finish_kernel)
     uint32_t wave_blocks;            // render_wave_kernel: CUs to fill with one resident set of blocks
+    uint32_t small_blocks;           // render_wave_kernel: 256-thread blocks (launches of < 2^24 paths)
     const vr4* bvh;
     const vr4* bvh4;                 // 4-wide nodes, 7 rows each (culled traversal, VR_BVH4)
     uint32_t n_nodes4;

@@ -933,7 +933,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // accumulates in place on `stream`.
         // Without overlap every launch uses the same path stream, so it waits
         // for the previous one (and its finish pass, below) like a single stream.
-        const bool ovl = c->overlap > 0 || (c->overlap < 0 && (size_t)p.path_stride * 2u * k < ((size_t)1 << 24));
+        const bool small = (size_t)p.path_stride * 2u * k < ((size_t)1 << 24);
+        const bool ovl = c->overlap > 0 || (c->overlap < 0 && small);
+        p.small_blocks = small ? 1u : 0u;
         if (!ovl) c->parity = 0;
         auto& l = c->lane[c->parity];
         hipStream_t rs = p.use_scratch ? l.s : c->stream;
