@@ -212,7 +212,8 @@ def main():
             "data": WORKLOADS[CFG][1],
             "config": {"workload": WORKLOADS[CFG][0], "width": W, "height": H, "frames_per_step": F,
                        "paths_per_step": paths_per_step, "parallelism": f"tile{world}",
-                       "gather": "RCCL gather of RGBA8 tiles to rank 0 per step" if world > 1 else "none"},
+                       "gather": ("RCCL" if backend == "nccl" else backend) + " gather of RGBA8 tiles to rank 0 per step"
+                       if world > 1 else "none"},
             "mrays_per_s": round(mrays, 3),
             "rays_per_path": round(rays_per_path, 4),
             "bytes_per_path": round(bytes_per_launch / max(own_paths, 1), 1),
