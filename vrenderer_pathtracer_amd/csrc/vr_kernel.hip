@@ -995,7 +995,7 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
 {
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
     // the path kernel's queue heads, for the next launch on this scratch
-    if (tile == 0 && tid < VR_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride] = 0u;
+    if (tile == 0 && tid < VR_MAX_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride] = 0u;
     const int wave = (int)tid >> 6, lane = (int)tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
     const uint32_t tile_y = gtile / p.tiles_x;
@@ -1281,18 +1281,17 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
 
     // Work queues: chunk c = (sub-tile c / n_paths, path c % n_paths), so the
     // paths of one sub-tile are handed out together (coherent rays, the
-    // sub-tile's primary records in cache).  VR_QUEUES heads, queue j hands
+    // sub-tile's primary records in cache).  p.n_queues heads, queue j hands
     // out chunks j, j + Q, j + 2Q, ... (one device-scope atomic per chunk; a
     // single head saturates: MI355X_MICROARCH "dequeue").  A wave draws from
     // its block's queue and, once that is drained, from the following ones.
     // With VR_XCD_BANDS (default 128 sub-tiles = 32 tiles) the sub-tiles are
     // dealt to the 8 XCDs in bands, so each XCD's L2 serves a coherent part of
     // the image (C2 +0.7 %, C3 +1.7 %, C5 +0.7 % over chunk-interleaved queues).
-    constexpr uint32_t Q = VR_QUEUES;
-    static_assert(Q % 8u == 0u, "VR_QUEUES must be a multiple of the 8 XCDs");
+    const uint32_t Q = p.n_queues;                         // power of two, multiple of the 8 XCDs
     const uint32_t n_chunks = n_sub * n_paths;
     (void)n_chunks;
-    uint32_t qj = blockIdx.x % Q, drained = 0;
+    uint32_t qj = blockIdx.x & (Q - 1u), drained = 0;
     auto grab = [&](uint32_t& sub, uint32_t& path) {       // wave-uniform; sub = ~0u when no work is left
         for (;;) {
             uint32_t v = 0;

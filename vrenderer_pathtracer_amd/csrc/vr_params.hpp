@@ -31,10 +31,20 @@ constexpr int kMaxFramesPerLaunch = 64;
 constexpr int kCounters = 8;
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
-// render_wave_kernel work queues: VR_QUEUES counters, kQueueStride uint32 apart
+// render_wave_kernel work queues: RenderParams::n_queues counters (a power of
+// two, multiple of 8), kQueueStride uint32 apart: VR_QUEUES for launches of
+// fewer than 2^25 paths, VR_QUEUES_LARGE above (C5-size launches dequeue
+// fastest: 64 heads +4 % there, while C2 / C3 frames and shards prefer 16)
 #ifndef VR_QUEUES
 #define VR_QUEUES 16
 #endif
+#ifndef VR_QUEUES_LARGE
+#define VR_QUEUES_LARGE 64
+#endif
+#define VR_MAX_QUEUES (VR_QUEUES > VR_QUEUES_LARGE ? VR_QUEUES : VR_QUEUES_LARGE)
+static_assert((VR_QUEUES & (VR_QUEUES - 1)) == 0 && VR_QUEUES % 8 == 0, "VR_QUEUES: power of two, multiple of 8");
+static_assert((VR_QUEUES_LARGE & (VR_QUEUES_LARGE - 1)) == 0 && VR_QUEUES_LARGE % 8 == 0,
+              "VR_QUEUES_LARGE: power of two, multiple of 8");
 constexpr uint32_t kQueueStride = 256;
 
 struct RenderParams {
@@ -53,6 +63,7 @@ struct RenderParams {
     uint32_t* chunk_ctr;             // render_wave_kernel's work queue heads (zeroed by finish_kernel)
     uint32_t wave_blocks;            // render_wave_kernel: CUs to fill with one resident set of blocks
     uint32_t small_blocks;           // render_wave_kernel: 256-thread blocks (launches of < 2^24 paths)
+    uint32_t n_queues;               // render_wave_kernel: work queue heads in use (VR_QUEUES / VR_QUEUES_LARGE)
     const vr4* bvh;
     const vr4* bvh4;                 // 4-wide nodes, 7 rows each (culled traversal, VR_BVH4)
     uint32_t n_nodes4;

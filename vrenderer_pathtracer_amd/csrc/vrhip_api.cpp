@@ -836,7 +836,7 @@ static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t p
         l.prim_cap = prim_need;
     }
     if (!l.chunk_ctr) {
-        const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * VR_QUEUES;
+        const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * VR_MAX_QUEUES;
         HIP_TRY(hipMalloc((void**)&l.chunk_ctr, bytes));
         HIP_TRY(hipMemsetAsync(l.chunk_ctr, 0, bytes, c->stream));
         HIP_TRY(hipEventRecord(c->ev_join, c->stream));
@@ -936,6 +936,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         const bool small = (size_t)p.path_stride * 2u * k < ((size_t)1 << 24);
         const bool ovl = c->overlap > 0 || (c->overlap < 0 && small);
         p.small_blocks = small ? 1u : 0u;
+        p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? VR_QUEUES : VR_QUEUES_LARGE;
         if (!ovl) c->parity = 0;
         auto& l = c->lane[c->parity];
         hipStream_t rs = p.use_scratch ? l.s : c->stream;
