@@ -237,6 +237,9 @@ int vrhip_selftest_math(int device, int fn, const float *a, const float *b, floa
  * [lo_bits, hi_bits) and its negation (test hook; hi_bits <= 2^31).
  * *mismatches = count, *first_bad = smallest mismatching pattern or ~0u. */
 int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t *mismatches, uint32_t *first_bad);
+/* The same for the kernels' square root (sqrt_rn: v_sqrt_f32 + the neighbour
+ * tests of the IEEE expansion) against sqrtf, positive patterns only. */
+int vrhip_selftest_sqrt(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t *mismatches, uint32_t *first_bad);
 
 /* ---- host-side helpers (no device needed) ----------------------------- */
 /* Native BVH build + reference flattening (src/vRendererCuda.cpp:204-279)

@@ -51,6 +51,7 @@ def test_null_context_is_invalid(native):
     assert native.vrhip_set_overlap(None, -1) == -1
     assert native.vrhip_set_path_split(None, 0) == -1
     assert native.vrhip_selftest_rcp(0, 0, 1, None, None) == -1
+    assert native.vrhip_selftest_sqrt(0, 0, 1, None, None) == -1
     assert native.vrhip_destroy(None) == 0
     assert native.vrhip_build_flat(None, None, None, None, 0, None, 0, 4, None, None, None, None, None, None,
                                    None) == -1

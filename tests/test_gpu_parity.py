@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import pyoracle as po
-from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math, selftest_rcp
+from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math, selftest_rcp, selftest_sqrt
 
 pytestmark = pytest.mark.gpu
 
@@ -105,6 +105,16 @@ def test_rcp_exhaustive(native):
     lo = int(np.float32(2.0 ** -32).view(np.uint32))
     hi = int(np.float32(2.0 ** 125).view(np.uint32)) + 1
     n, first = selftest_rcp(lo, hi)
+    assert n == 0, f"{n} mismatches, first {first:#010x}"
+
+
+def test_sqrt_exhaustive(native):
+    # sqrt_rn (vr_math.hpp; sphere tests, normalisation, cosine sampling)
+    # equals sqrtf for every float in [2^-96, FLT_MAX] (1.9e9 inputs); waves
+    # with an input outside take sqrtf
+    lo = int(np.float32(2.0 ** -96).view(np.uint32))
+    hi = 0x7f800000
+    n, first = selftest_sqrt(lo, hi)
     assert n == 0, f"{n} mismatches, first {first:#010x}"
 
 

@@ -81,6 +81,8 @@ _SIGNATURES = {
     "vrhip_selftest_math": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _f, _f, _f, ctypes.c_size_t]),
     "vrhip_selftest_rcp": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.POINTER(ctypes.c_uint64), _u32]),
+    "vrhip_selftest_sqrt": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.c_uint64), _u32]),
     "vrhip_build_flat": (ctypes.c_int, [_f, _f, _f, _f, ctypes.c_uint32, _u32, ctypes.c_uint32, ctypes.c_uint32,
                                         _f, _sz, _f, _f, _f, _f, _sz]),
     "vrhip_validate_flat": (ctypes.c_int, [_f, ctypes.c_size_t, _f, ctypes.c_size_t, _u32, _u32]),

@@ -54,7 +54,7 @@ __device__ __forceinline__ float dot4(vr4 a, vr4 b) { return a.x * b.x + a.y * b
 __device__ __forceinline__ vr4 cross4(vr4 a, vr4 b) {
     return mk4(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x, 0.0f);
 }
-__device__ __forceinline__ vr4 normalize4(vr4 a) { const float inv = 1.0f / __builtin_sqrtf(dot4(a, a)); return mul4s(a, inv); }
+__device__ __forceinline__ vr4 normalize4(vr4 a) { const float inv = inv_sqrt_exact(dot4(a, a)); return mul4s(a, inv); }
 __device__ __forceinline__ float clampi(int v, int lo, int hi) { const int m = hi < v ? hi : v; return (float)(lo > m ? lo : m); }
 __device__ __forceinline__ float clampf(float v, float lo, float hi) { return __builtin_fmaxf(lo, __builtin_fminf(hi, v)); }
 __device__ __forceinline__ vr4 tbn_mul(vr4 m0, vr4 m1, vr4 m2, vr4 b) {   // mat4 * float4, m3 = (0,0,0,1)
@@ -102,7 +102,7 @@ __device__ __forceinline__ float sphere_intersect(const Sph& s, const Ray& r) {
     const float b = dot4(op, r.d);
     float det = b * b - dot4(op, op) + s.r * s.r;
     if (det < 0) return 0;
-    det = __builtin_sqrtf(det);
+    det = sqrt_exact(det);
     float t;
     return (t = b - det) > eps ? t : ((t = b + det) > eps ? t : 0.0f);
 }
@@ -878,7 +878,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
     }
     if (ps.bounce == 0) {
         const vr4 l = sub4(ray.o, h.hp);
-        ps.depth = __builtin_sqrtf(dot4(l, l)) / 150.f;
+        ps.depth = sqrt_exact(dot4(l, l)) / 150.f;
     }
     ps.accum = add4(ps.accum, mul4(ps.mask, h.em));
     ray.o = h.hp;
@@ -905,13 +905,13 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         } else {
             const float rand1 = 2.f * VR_PI * ps.rng.uniform();
             const float rand2 = ps.rng.uniform();
-            const float rand2s = __builtin_sqrtf(rand2);
+            const float rand2s = sqrt_exact(rand2);
             const vr4 u = normalize4(cross4(axis, w));
             const vr4 v = cross4(w, u);
             float sn, cs;
             sincos_p(rand1, &sn, &cs);
             newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
-                                     mul4s(w, __builtin_sqrtf(1 - rand2))));
+                                     mul4s(w, sqrt_exact(1 - rand2))));
             muleq4(ps.mask, h.col);
             muleq4s(ps.mask, dot4(newdir, normal));
             muleq4s(ps.mask, 2.f);
@@ -923,13 +923,13 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
         const float rand1 = 2.f * VR_PI * ps.rng.uniform();
         const float rand2 = ps.rng.uniform();
-        const float rand2s = __builtin_sqrtf(rand2);
+        const float rand2s = sqrt_exact(rand2);
         const vr4 u = normalize4(cross4(axis, w));
         const vr4 v = cross4(w, u);
         float sn, cs;
         sincos_p(rand1, &sn, &cs);
         const vr4 newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
-                                           mul4s(w, __builtin_sqrtf(1 - rand2))));
+                                           mul4s(w, sqrt_exact(1 - rand2))));
         if HAS(F_BRDF) {
             const float dw = 24 * pow_p(newdir.x * newdir.x + newdir.y * newdir.y + newdir.z * newdir.z, -1.5f);
             if (COUNT) cnt.brdf++;
@@ -1615,20 +1615,22 @@ int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t 
     return (int)hipGetLastError();
 }
 
-// Exhaustive check of rcp_rn against IEEE division over the float bit
-// patterns [lo, hi) of both signs: counts mismatches, records the smallest
+// Exhaustive checks of the short sequences against the IEEE operations over
+// float bit patterns [lo, hi): fn 0 rcp_rn vs 1.f / x (both signs), fn 1
+// sqrt_rn vs sqrtf (positive x).  Counts mismatches, records the smallest
 // mismatching pattern.
-__global__ void selftest_rcp_kernel(uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad)
+__global__ void selftest_exact_kernel(int fn, uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad)
 {
     const uint32_t stride = gridDim.x * blockDim.x;        // hi <= 2^31: b + stride cannot wrap
     unsigned long long bad = 0;
     uint32_t first = 0xffffffffu;
     for (uint32_t b = lo + blockIdx.x * blockDim.x + threadIdx.x; b < hi; b += stride) {
-#pragma unroll
-        for (int neg = 0; neg < 2; ++neg) {
+        for (int neg = 0; neg < (fn == 0 ? 2 : 1); ++neg) {
             const uint32_t bits = neg ? (b | 0x80000000u) : b;
             const float x = __uint_as_float(bits);
-            if (__float_as_uint(rcp_rn(x)) != __float_as_uint(1.f / x)) {
+            const float got = fn == 0 ? rcp_rn(x) : sqrt_rn(x);
+            const float want = fn == 0 ? 1.f / x : __builtin_sqrtf(x);
+            if (__float_as_uint(got) != __float_as_uint(want)) {
                 ++bad;
                 first = bits < first ? bits : first;
             }
@@ -1640,9 +1642,11 @@ __global__ void selftest_rcp_kernel(uint32_t lo, uint32_t hi, unsigned long long
     }
 }
 
-int launch_selftest_rcp(uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad, void* stream)
+int launch_selftest_exact(int fn, uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad,
+                          void* stream)
 {
-    hipLaunchKernelGGL(selftest_rcp_kernel, dim3(4096), dim3(256), 0, (hipStream_t)stream, lo, hi, n_bad, first_bad);
+    hipLaunchKernelGGL(selftest_exact_kernel, dim3(4096), dim3(256), 0, (hipStream_t)stream, fn, lo, hi, n_bad,
+                       first_bad);
     return (int)hipGetLastError();
 }
 

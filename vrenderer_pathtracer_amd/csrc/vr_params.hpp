@@ -95,6 +95,7 @@ int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);
 int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,
                       uint32_t n_owned, uint32_t rank, uint32_t nranks, int unpack, void* stream);
 int launch_selftest_math(int fn, const float* a, const float* b, float* out, size_t n, void* stream);
-int launch_selftest_rcp(uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad, void* stream);
+int launch_selftest_exact(int fn, uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad,
+                          void* stream);
 
 } // namespace vr

@@ -1173,7 +1173,8 @@ int vrhip_selftest_math(int device, int fn, const float* a, const float* b, floa
     return VRHIP_OK;
 }
 
-int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches, uint32_t* first_bad)
+static int selftest_exact(int fn, int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
+                          uint32_t* first_bad)
 {
     if (!mismatches || !first_bad) return fail(VRHIP_ERR_INVALID, "null argument");
     if (lo_bits > hi_bits || hi_bits > 0x80000000u) return fail(VRHIP_ERR_INVALID, "bit range outside [0, 2^31]");
@@ -1184,7 +1185,7 @@ int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t*
     const uint32_t init_first = 0xffffffffu;
     HIP_TRY(hipMemset(d, 0, 8));
     HIP_TRY(hipMemcpy(df, &init_first, 4, hipMemcpyHostToDevice));
-    int e = vr::launch_selftest_rcp(lo_bits, hi_bits, d, df, nullptr);
+    int e = vr::launch_selftest_exact(fn, lo_bits, hi_bits, d, df, nullptr);
     if (e) { (void)hipFree(d); return fail(VRHIP_ERR_HIP, "selftest launch failed"); }
     unsigned long long n = 0;
     HIP_TRY(hipMemcpy(&n, d, 8, hipMemcpyDeviceToHost));
@@ -1192,6 +1193,16 @@ int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t*
     (void)hipFree(d);
     *mismatches = n;
     return VRHIP_OK;
+}
+
+int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches, uint32_t* first_bad)
+{
+    return selftest_exact(0, device, lo_bits, hi_bits, mismatches, first_bad);
+}
+
+int vrhip_selftest_sqrt(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches, uint32_t* first_bad)
+{
+    return selftest_exact(1, device, lo_bits, hi_bits, mismatches, first_bad);
 }
 
 int vrhip_build_flat(const float* positions, const float* normals, const float* tangents, const float* uvs,

@@ -397,6 +397,16 @@ def selftest_rcp(lo_bits: int, hi_bits: int, device: int = 0):
     return int(n.value), int(first.value)
 
 
+def selftest_sqrt(lo_bits: int, hi_bits: int, device: int = 0):
+    """Exhaustively compare the kernels' square root with sqrtf over the float
+    bit patterns [lo_bits, hi_bits): (mismatches, first_bad)."""
+    n = ctypes.c_uint64(0)
+    first = ctypes.c_uint32(0)
+    check(_native.lib().vrhip_selftest_sqrt(device, lo_bits, hi_bits, ctypes.byref(n), ctypes.byref(first)),
+          "vrhip_selftest_sqrt")
+    return int(n.value), int(first.value)
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     rc = _native.lib().vrhip_device_count(ctypes.byref(n))
