@@ -253,9 +253,18 @@ __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, f
     L.stk[0] = kSentinel;
     tr.top = kSentinel;
     tr.nodeAddr = 0;
-    tr.ivx = 1.f / (__builtin_fabsf(r.d.x) > VR_EPS ? r.d.x : VR_EPS);
-    tr.ivy = 1.f / (__builtin_fabsf(r.d.y) > VR_EPS ? r.d.y : VR_EPS);
-    tr.ivz = 1.f / (__builtin_fabsf(r.d.z) > VR_EPS ? r.d.z : VR_EPS);
+    // invDir (PathTracer.cu:289-294): components with |d| <= eps become +eps,
+    // so |d| >= eps > 2^-32 and rcp_rn is the IEEE quotient unless a
+    // component exceeds 2^125 (then the wave divides)
+    const float dx = __builtin_fabsf(r.d.x) > VR_EPS ? r.d.x : VR_EPS;
+    const float dy = __builtin_fabsf(r.d.y) > VR_EPS ? r.d.y : VR_EPS;
+    const float dz = __builtin_fabsf(r.d.z) > VR_EPS ? r.d.z : VR_EPS;
+    if (__builtin_expect(__ballot(!(__builtin_fabsf(dx) <= kRcpRnHi && __builtin_fabsf(dy) <= kRcpRnHi &&
+                                    __builtin_fabsf(dz) <= kRcpRnHi)) != 0ull, 0)) {
+        tr.ivx = 1.f / dx; tr.ivy = 1.f / dy; tr.ivz = 1.f / dz;
+    } else {
+        tr.ivx = rcp_rn(dx); tr.ivy = rcp_rn(dy); tr.ivz = rcp_rn(dz);
+    }
     tr.odx = r.o.x * tr.ivx; tr.ody = r.o.y * tr.ivy; tr.odz = r.o.z * tr.ivz;
     tr.t = t0;
     // t-culling: a child whose slab entry lies beyond the closest hit so far
