@@ -4,88 +4,188 @@
 Workload (BASELINE.json configs[1], SURVEY.md 8d "C2"): Cornell box + 10k-tri
 torus knot, diffuse only, 1280x720, 2 paths/pixel/frame, 4 bounces, default
 camera, Fresnel 0.1/3.0.  One "step" = one progressive accumulation step of
-FRAMES_PER_STEP frames over the whole 1280x720 image (inputs resident in
-HBM), ending with the tile gather to rank 0 when N > 1.
+FRAMES_PER_STEP frames over the whole image (inputs resident in HBM), ending
+with the tile gather to rank 0 when N > 1.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F] [--config C2]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F] [--config C1..C5]
 
---config C3 / C5 runs the same measurement on another BASELINE.json
-configuration (C3: HDRI + textured knot at 1280x720; C5: 1M-triangle knot
-under HDRI at 3840x2160); the default and the number of record is C2.
+--config runs the same measurement on another BASELINE.json configuration
+(C1 Cornell + example sphere 512x512, C3 HDRI + textured knot 1280x720, C4
+MERL BRDF sphere under HDRI 1920x1080, C5 1M-triangle knot under HDRI
+3840x2160); the default and the number of record is C2.
 
-N > 1: one process per GPU (torch.distributed.run), 16x16 pixel
-tiles dealt round-robin, each rank renders its tiles of every frame, then one
-RCCL gather (torch.distributed over "nccl" = RCCL) of the RGBA8 tiles to rank
-0 per step.
-Strong scaling: the frame size is fixed.
+N > 1: one process per GPU.  Without an external launcher (WORLD_SIZE unset)
+this process starts `torch.distributed.run` with N ranks as a CHILD process
+(it never touches the GPU itself) and exits with the child's status.  16x16
+pixel tiles are dealt round-robin; each rank renders its tiles of every frame,
+then one RCCL gather (ncclGather through the library's C ABI,
+vrhip_comm_gather) brings the RGBA8 tiles to rank 0 per step.  Strong scaling:
+the frame size is fixed.
 
 Prints ONE JSON line (rank 0).  value = total paths of all ranks / max-over-
-ranks wall time of the K timed steps.  roofline = the render
-kernels' algorithmic bytes per launch (counted by the kernel's counting
-variant on a separate, untimed step; SURVEY.md 8d byte costs) / their
-average launch time (HIP events around primary_kernel + render_wave_kernel
-on the path stream they run on, inside the timed region).  cpu_baseline =
-the CPU oracle (oracle/, a C restatement of the reference kernel) on a
-bounded sample of the same workload on this host's cores.
+ranks wall time of the K timed steps.  "interactive" = the same config one
+frame per synchronous call (the reference's render() cadence,
+src/vRendererCuda.cpp:107-165).  roofline = the render kernels' EXECUTED
+global-load bytes per launch (counted by the instrumented copy of the
+production kernels, vrhip_render_profiled, on a separate untimed step) over
+their average launch time (HIP events around primary_kernel +
+render_wave_kernel on the path stream they run on, inside the timed region),
+against the vector-memory gather roof measured live on this GPU
+(vrhip_microbench_vmem), the L2 peak and the HBM peak (physical HBM bytes
+from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes in profiles/).  The reference
+algorithm's bytes (SURVEY.md 8d pricing) are reported separately.
+cpu_baseline = the CPU oracle (oracle/, a C restatement of the reference
+kernel) on a bounded sample of the same workload on this host's cores.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md "HBM": 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate
+METRIC = "Mpaths/sec (+ Mrays/sec) at 1280x720 progressive; 1/2/4/8 MI355X"
 WORKLOADS = {
+    "C1": ("C1: Cornell box + example sphere, 512x512, 2 spp/frame, 4 bounces",
+           "synthetic (procedural Cornell box + example sphere; SURVEY.md 8d C1)"),
     "C2": ("C2: Cornell box + 10k-tri torus knot, diffuse, 1280x720, 2 spp/frame, 4 bounces",
            "synthetic (procedural Cornell box + 10k-tri torus knot; SURVEY.md 8d C2)"),
     "C3": ("C3: HDRI env + 10k-tri torus knot with diffuse/normal/specular maps + Fresnel, 1280x720, "
            "2 spp/frame, 4 bounces",
            "synthetic (procedural 2048x1024 HDRI, 1024^2 maps, 10k-tri torus knot; SURVEY.md 8d C3)"),
+    "C4": ("C4: MERL BRDF on the example sphere under HDRI, 1920x1080 (rendered 1920x1072), 2 spp/frame, 4 bounces",
+           "synthetic (procedural 2048x1024 HDRI, analytic lobe sampled on the MERL grid; SURVEY.md 8d C4)"),
     "C5": ("C5: 1M-tri torus knot (SBVH-depth tree) under HDRI, 3840x2160, 2 spp/frame, 4 bounces",
            "synthetic (procedural 2048x1024 HDRI, 1M-tri torus knot; SURVEY.md 8d C5)"),
 }
-PROFILE_TRAFFIC = os.path.join(REPO, "profiles", "traffic_c2.json")
 
 
-def algorithmic_bytes(c: dict, paths: int, pixel_frames: int) -> float:
-    """SURVEY.md 8d byte costs, as the kernel executes them: 64 B/node visit,
-    48 B/triangle tested (16 B per terminator slot read, 0 with the device
-    layout), hit attribute bytes, 16 B/texture or HDRI fetch, 12 B/BRDF lookup,
-    92 B of pixel I/O per pixel-frame."""
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """Start n ranks (one per GPU) under torch.distributed.run as a child
+    process; this process never initialises the GPU (no exec after GPU use)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+# ---- bytes ------------------------------------------------------------------
+def reference_bytes(c: dict, paths: int, pixel_frames: int) -> float:
+    """SURVEY.md 8d byte costs of the REFERENCE algorithm (strict traversal, no
+    primary-hit reuse): 64 B/node visit, 48 B/triangle tested (+16 B per
+    terminator slot read, 0 with the device layout), hit attribute bytes,
+    16 B/texture or HDRI fetch, 12 B/BRDF lookup, 92 B of pixel I/O per pixel-frame."""
     return (64 * c["node_visits"] + 16 * c["slot_reads"] + 48 * c["tri_tests"] + c["attr_bytes"]
             + 16 * c["tex_fetches"] + 16 * c["hdr_fetches"] + 12 * c["brdf_fetches"] + 92 * pixel_frames)
 
 
-def cpu_baseline(scene: dict, budget_s: float, threads: int) -> dict:
+def executed_loads(e: dict, paths: int, wave_kernel: bool) -> dict:
+    """Per-lane global loads the production render kernels issue, by width
+    (bytes): node rows 3x16 + child indices 8 per node visit not served from
+    LDS; triangles 3x12 (v0, two edges) per triangle load; per mesh hit shaded
+    uv 3x8 + tangents 3x16 + normals 3x16 (normal map) or vertices 3x12 (face
+    normal); 16 per texture / HDRI texel; 3x4 per BRDF lookup; 2x16 primary
+    record per path (path kernel)."""
+    glob = e["node_visits"] - e["node_visits_lds"]
+    hits, nmap = e["mesh_hits"], e["nmap_hits"]
+    return {16: 3 * glob + 3 * hits + 3 * nmap + e["tex_fetches"] + e["hdr_fetches"] + (2 * paths if wave_kernel else 0),
+            12: 3 * e["tri_loads"] + 3 * (hits - nmap),
+            8: glob + 3 * hits,
+            4: 3 * e["brdf_fetches"]}
+
+
+def vmem_roof(device: int) -> dict:
+    """Lane loads/s of the vector-memory gather path per load width: the best
+    over 1..64 distinct addresses per wave-instruction (vrhip_microbench_vmem)."""
+    from vrenderer_pathtracer_amd import microbench_vmem
+    roof = {}
+    for w in (16, 12, 8, 4):
+        rates = {d: microbench_vmem(w, d, device) for d in (1, 4, 16, 64)}
+        roof[w] = {"best": max(rates.values()), "by_distinct": {str(d): round(r / 1e9, 2) for d, r in rates.items()}}
+    return roof
+
+
+def hbm_traffic(cfg: str):
+    """Physical HBM bytes per render launch of bench.py's step on this config
+    (rocprofv3 2*FETCH_SIZE + WRITE_SIZE of primary_kernel + render_wave_kernel,
+    profiles/traffic_<cfg>.json, MI355X_MICROARCH.md HBM corrections)."""
+    path = os.path.join(REPO, "profiles", f"traffic_{cfg.lower()}.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        d = json.load(open(path))
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
+    except Exception:
+        return None, None
+
+
+# ---- CPU baseline -------------------------------------------------------------
+def cpu_info() -> dict:
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = aff
+    why = f"sched_getaffinity = {aff} CPUs"
+    if omp and omp.isdigit() and 0 < int(omp) < aff:
+        threads = int(omp)
+        why += f"; OMP_NUM_THREADS = {omp} (the lease's CPU share)"
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": aff, "threads": threads, "threads_why": why}
+
+
+def cpu_baseline(scene: dict, budget_s: float) -> dict:
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import pyoracle
     pyoracle.build()
+    info = cpu_info()
+    threads = info["threads"]
     W, H = scene["width"], scene["height"]
+    hr = (H // 16) * 16
     accum = np.zeros((H, W, 4), np.float32)
     paths, frames, t0 = 0, 0, time.perf_counter()
     chunk = 16
     while time.perf_counter() - t0 < budget_s and frames < 64:
         frame = frames + 1
-        for r0 in range(0, H, chunk):
+        for r0 in range(0, hr, chunk):
             pyoracle.render(scene, frames=1, times=[scene["time"] + frames], first_frame=frame,
-                            rows=(r0, min(H, r0 + chunk)), threads=threads, accum=accum)
-            paths += (min(H, r0 + chunk) - r0) * W * 2
+                            rows=(r0, min(hr, r0 + chunk)), threads=threads, accum=accum)
+            paths += (min(hr, r0 + chunk) - r0) * (W // 16) * 16 * 2
             if time.perf_counter() - t0 >= budget_s:
                 break
         frames += 1
     dt = time.perf_counter() - t0
-    rows = paths // (2 * W)
-    return {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ C restatement (glibc libm, -O2, OpenMP {threads} threads), {scene['name']} "
-                      f"{W}x{H}, {rows} rows over {frames} frame(s) ({paths} paths, {dt:.1f} s)"}
+    rows = paths // (2 * (W // 16) * 16)
+    out = {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/ C restatement (glibc libm, -O2, OpenMP {threads} threads), {scene['name']} "
+                     f"{W}x{H}, {rows} rows over {frames} frame(s) ({paths} paths, {dt:.1f} s)"}
+    out.update(info)
+    return out
 
 
+# ---- main ---------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,28 +194,52 @@ def main():
     ap.add_argument("--frames-per-step", type=int, default=16)
     ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--interactive-frames", type=int, default=30,
+                    help="frames of the one-frame-per-call measurement (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-roof", action="store_true", help="skip the vector-memory roof micro-benchmark")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="form the process group over gloo, count the ranks and exit (no GPU; tests the launcher)")
     args = ap.parse_args()
 
-    import numpy as np
-    import torch
-    import torch.distributed as dist
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+
+    if args.check_launch:
+        if world > 1:
+            dist.init_process_group("gloo")
+        n = torch.ones(1)
+        if world > 1:
+            dist.all_reduce(n)
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"check_launch": True, "n_gpus": int(n.item()), "gpus_arg": args.gpus}), flush=True)
+        return
+
     # VRHIP_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
-    # on one GPU (host-staged gather); the measured configuration is "nccl"
-    # (RCCL over xGMI), one rank per GPU
+    # on one GPU (host-staged gather); the measured configuration is "nccl":
+    # one rank per GPU, the tile gather over RCCL (xGMI) in the C ABI
     backend = os.environ.get("VRHIP_DIST_BACKEND", "nccl")
     gpu = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", gpu)
+    torch.cuda.set_device(gpu)
     if world > 1:
-        torch.cuda.set_device(gpu)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        formed = dist.get_world_size()
+        if formed != args.gpus:
+            raise SystemExit(f"bench.py: process group formed {formed} ranks, --gpus {args.gpus}")
     red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from vrenderer_pathtracer_amd import VRendererHIP, build_native, scenes
@@ -128,22 +252,26 @@ def main():
 
     r = VRendererHIP(gpu)
     scenes.load_into(r, scene)
-    # one non-default stream shared by the renderer and torch (the collective
-    # is ordered after the pack kernel by torch's stream semantics)
-    stream = torch.cuda.Stream(device=dev)
-    torch.cuda.set_stream(stream)
-    r.set_stream(stream.cuda_stream)
     r.set_tiling(rank, world)
     owned = r.owned_pixels()
     gather = TileGather(r, rank, world, dev, WHAT_RGBA8)
+    mesh = scene.get("mesh_flat") is not None
 
-    # counting step (untimed): exact event counts of the REFERENCE algorithm for
-    # this rank's share (strict traversal; the counting variant also skips the
-    # primary-hit reuse and last-bounce shortcut), i.e. the algorithmic work
+    # untimed counting steps on this rank's share: (1) the reference
+    # algorithm's events (strict traversal, no primary-hit reuse, no last-
+    # bounce shortcut) for the survey's byte pricing and Mrays/s; (2) the
+    # memory operations the production kernels execute, for the roofline
     r.set_strict_traversal(True)
-    counts = r.render_counted(frames=F, time_seed=scene["time"])
+    ref_counts = r.render_counted(frames=F, time_seed=scene["time"])
     r.set_strict_traversal(False)
     r.clearBuffer()
+    exec_counts = r.render_profiled(frames=F, time_seed=scene["time"])
+    r.clearBuffer()
+    r.sync()
+
+    roof = None
+    if rank == 0 and not args.no_roof:
+        roof = vmem_roof(gpu)
 
     def step(i):
         times = [scene["time"] + i * F + k for k in range(F)]
@@ -152,6 +280,7 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    r.sync()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -160,6 +289,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+    r.sync()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -170,9 +300,38 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    # interactive cadence: one frame per synchronous render() call (+ gather)
+    inter = None
+    if args.interactive_frames > 0:
+        r.clearBuffer()
+        base = scene["time"] + 100000
+        for i in range(3):
+            r.render(frames=1, times=[base + i], sync=True)
+            gather.step()
+        r.sync()
+        if world > 1:
+            dist.barrier()
+        ti = time.perf_counter()
+        for i in range(args.interactive_frames):
+            r.render(frames=1, times=[base + 3 + i], sync=True)
+            gather.step()
+            r.sync()
+        if world > 1:
+            dist.barrier()
+        te = torch.tensor([time.perf_counter() - ti], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        te = float(te.item())
+        pf = (W // 16) * 16 * (H // 16) * 16 * 2
+        inter = {"frames_per_step": 1, "frames": args.interactive_frames,
+                 "value": round(pf * args.interactive_frames / te / 1e6, 3), "unit": "Mpaths/s",
+                 "ms_per_frame": round(te / args.interactive_frames * 1e3, 4),
+                 "note": "one frame per synchronous render() call (src/vRendererCuda.cpp:107-165 syncs every "
+                         "frame)" + (", plus the RGBA8 tile gather to rank 0 per frame" if world > 1 else "")}
+
     # aggregate counts over ranks
-    keys = sorted(counts)
-    cvec = torch.tensor([counts[k] for k in keys] + [owned], dtype=torch.float64, device=red_dev)
+    keys = sorted(ref_counts)
+    cvec = torch.tensor([ref_counts[k] for k in keys] + [owned], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(cvec)
     tot = {k: float(v) for k, v in zip(keys + ["owned_pixels"], cvec.tolist())}
@@ -186,19 +345,48 @@ def main():
     mrays = value * rays_per_path
 
     if rank == 0:
-        # roofline of the render kernel on rank 0 (its own share per launch)
         own_paths = owned * 2 * F
-        bytes_per_launch = algorithmic_bytes(counts, own_paths, owned * F)
         avg_launch_s = (kms / 1e3) / max(launches, 1)
-        achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        traffic = None
-        if CFG == "C2" and os.path.exists(PROFILE_TRAFFIC):   # rocprofv3 PMC of the C2 step
-            try:
-                traffic = json.load(open(PROFILE_TRAFFIC)).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        loads = executed_loads(exec_counts, own_paths, mesh)
+        load_bytes = sum(w * n for w, n in loads.items())
+        lds_bytes = 56 * exec_counts["node_visits_lds"]
+        store_bytes = 16 * own_paths + (32 * owned if mesh else 0)
+        ref_b = reference_bytes(ref_counts, own_paths, owned * F)
+        achieved = load_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        roofs = {}
+        if roof:
+            t_min = sum(n / roof[w]["best"] for w, n in loads.items())
+            roofs["vmem"] = {"achieved": round(achieved, 1), "peak": round(load_bytes / t_min / 1e9, 1),
+                             "frac": round(t_min / avg_launch_s, 4)}
+        roofs["l2"] = {"achieved": round(achieved, 1), "peak": L2_PEAK_GBS, "frac": round(achieved / L2_PEAK_GBS, 4)}
+        traffic, traffic_src = hbm_traffic(CFG)
+        if traffic and world == 1:
+            hbm_gbs = traffic / avg_launch_s / 1e9
+            roofs["hbm"] = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(hbm_gbs / HBM_PEAK_GBS, 4)}
+        bound = max(roofs, key=lambda k: roofs[k]["frac"])
+        roofline = {"bound": bound, "achieved": roofs[bound]["achieved"], "peak": roofs[bound]["peak"], "unit": "GB/s",
+                    "frac": roofs[bound]["frac"], "traffic": traffic if world == 1 else None,
+                    "kernel": "primary_kernel+render_wave_kernel" if mesh else "render_kernel",
+                    "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches": launches,
+                    "executed_load_bytes_per_launch": int(load_bytes),
+                    "lane_loads_per_launch": {f"b{8 * w}": int(n) for w, n in loads.items()},
+                    "lds_node_bytes_per_launch": int(lds_bytes), "store_bytes_per_launch": int(store_bytes),
+                    "roofs": roofs,
+                    "traffic_source": traffic_src,
+                    "vmem_roof_lane_loads_per_ns": ({f"b{8 * w}": v["by_distinct"] for w, v in roof.items()}
+                                                    if roof else None),
+                    "reference_algorithm": {
+                        "bytes_per_path": round(ref_b / max(own_paths, 1), 1),
+                        "gbs_at_this_rate": round(ref_b / avg_launch_s / 1e9, 1) if avg_launch_s > 0 else None,
+                        "note": "SURVEY 8d pricing of the reference algorithm's events (strict traversal, no "
+                                "primary-hit reuse); not executed bytes, so not a roofline"},
+                    "note": "achieved = global-load bytes the production kernels execute (instrumented copy, "
+                            "untimed step) / render-kernel launch time; vmem peak = the same lane loads at the "
+                            "live-measured gather roof (vrhip_microbench_vmem, best of 1..64 addresses per "
+                            "wave-instruction); bound = the roof with the largest fraction; traffic = physical "
+                            "HBM bytes per launch (rocprofv3 PMC, traffic_source)"}
         out = {
-            "metric": "Mpaths/sec (+ Mrays/sec) at 1280x720 progressive; 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mpaths/s",
             "n_gpus": world,
@@ -212,26 +400,20 @@ def main():
             "data": WORKLOADS[CFG][1],
             "config": {"workload": WORKLOADS[CFG][0], "width": W, "height": H, "frames_per_step": F,
                        "paths_per_step": paths_per_step, "parallelism": f"tile{world}",
-                       "gather": ("RCCL" if backend == "nccl" else backend) + " gather of RGBA8 tiles to rank 0 per step"
-                       if world > 1 else "none"},
+                       "gather": (("RCCL ncclGather (C ABI vrhip_comm_gather)" if backend == "nccl" else
+                                   backend + " gather (host-staged rehearsal)")
+                                  + " of RGBA8 tiles to rank 0 per step") if world > 1 else "none"},
             "mrays_per_s": round(mrays, 3),
             "rays_per_path": round(rays_per_path, 4),
-            "bytes_per_path": round(bytes_per_launch / max(own_paths, 1), 1),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "primary_kernel+render_wave_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                         "launches": launches,
-                         "note": "algorithmic bytes of the reference algorithm (SURVEY 8d), served mostly from "
-                                 "L2/LDS (traffic = physical HBM bytes per launch); launches of fewer than 2^24 paths "
-                                 "(sharded frames) overlap on three path streams, and then avg_launch_ms includes "
-                                 "time shared with the neighbouring launch"},
+            "interactive": inter,
+            "roofline": roofline,
         }
         if not args.no_cpu and world == 1:
-            threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(scene, args.cpu_budget, threads)
+            out["cpu_baseline"] = cpu_baseline(scene, args.cpu_budget)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    gather.close()
     r.cleanUp()
     if world > 1:
         dist.destroy_process_group()

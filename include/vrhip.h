@@ -29,7 +29,8 @@ typedef enum vrhip_status {
     VRHIP_ERR_NO_ENV = -3,       /* HDRI mode with no environment loaded */
     VRHIP_ERR_BVH = -4,          /* malformed or too-deep flattened BVH */
     VRHIP_ERR_NO_DEVICE = -5,
-    VRHIP_ERR_NOMEM = -6
+    VRHIP_ERR_NOMEM = -6,
+    VRHIP_ERR_COMM = -7          /* RCCL error (see vrhip_last_error) */
 } vrhip_status;
 
 /* vTextureType, cuda/include/PathTracer.cuh:86 */
@@ -160,6 +161,20 @@ int vrhip_render(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint3
  * (12 B).  Synchronous. */
 int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
                          uint64_t counters[8]);
+/* Same render as vrhip_render -- the production kernels' algorithm (t-culled
+ * traversal unless strict, primary hit shared by a pixel's paths, last bounce
+ * without material sampling), launch shape and results -- through an
+ * instrumented instantiation that counts the memory operations those kernels
+ * issue (the roofline's executed bytes; no reference counterpart).
+ * counters[0..7] as vrhip_render_counted but for the executed work
+ * (attribute bytes include the 36 B of vertices a mesh hit's face normal
+ * reads), then [8] node visits served from the block's LDS copy of the tree
+ * top (the rest read 3x16 B + 8 B from memory), [9] triangle loads issued
+ * (36 B each; an odd leaf's last pair loads its triangle twice), [10] mesh
+ * hits shaded, [11] of those through the normal map.  Synchronous. */
+#define VRHIP_PROFILE_COUNTERS 12
+int vrhip_render_profiled(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
+                          uint64_t counters[VRHIP_PROFILE_COUNTERS]);
 int vrhip_sync(vrhip_ctx *ctx);
 /* Path groups per pixel for vrhip_render in sphere-only scenes (no
  * reference counterpart: a launch shape knob; mesh scenes use the persistent
@@ -212,6 +227,30 @@ int vrhip_pack_tiles(vrhip_ctx *ctx, int what, void *dst_device);
  * tightly packed) into this context's full image `what`. */
 int vrhip_unpack_tiles(vrhip_ctx *ctx, int what, const void *src_device, uint32_t n_ranks, size_t stride_bytes);
 
+/* ---- multi-GPU tile gather over RCCL (xGMI) ----------------------------- */
+/* The reference is single-GPU; its per-pixel seeds use global pixel
+ * coordinates (cuda/src/PathTracer.cu:817-818), so ranks rendering disjoint
+ * tile sets reproduce the 1-GPU image bit for bit.  One process (or thread)
+ * per GPU, one context per rank:
+ *   rank 0: vrhip_comm_unique_id(id); hand `id` to every rank out of band
+ *   (MPI, a file, a socket, torch.distributed ...);
+ *   every rank: vrhip_comm_init(ctx, rank, n, id) -- joins the communicator
+ *   (ncclCommInitRank: blocks until all n ranks have called it) and sets the
+ *   tiling (vrhip_set_tiling(ctx, rank, n));
+ *   per accumulation step, after vrhip_render: vrhip_comm_gather(ctx, what).
+ * VRHIP_COMM_ID_BYTES = sizeof(ncclUniqueId). */
+#define VRHIP_COMM_ID_BYTES 128
+int vrhip_comm_unique_id(uint8_t id[VRHIP_COMM_ID_BYTES]);
+int vrhip_comm_init(vrhip_ctx *ctx, uint32_t rank, uint32_t n_ranks, const uint8_t id[VRHIP_COMM_ID_BYTES]);
+/* Every rank packs its tiles of image `what` (0 RGBA8, 1 float4 accumulation,
+ * 2 depth8), ONE ncclGather brings them to rank 0, and rank 0 scatters them
+ * into its full image -- all enqueued on the context stream behind the
+ * render's finish passes (no host synchronisation).  Rank 0's image `what`
+ * then holds the whole frame. */
+int vrhip_comm_gather(vrhip_ctx *ctx, int what);
+/* Leaves the communicator (waits for the context stream first).  vrhip_destroy does it too. */
+int vrhip_comm_destroy(vrhip_ctx *ctx);
+
 /* ---- diagnostics ------------------------------------------------------ */
 /* Kernel time of the last vrhip_render (ms, HIP events on the context stream;
  * requires vrhip_sync first). */
@@ -223,6 +262,15 @@ int vrhip_last_kernel_ms(vrhip_ctx *ctx, float *ms);
  * span includes time shared with the neighbouring launch.  Waits for the
  * pending launches. */
 int vrhip_kernel_stats(vrhip_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
+/* Vector-memory gather roof of `device` (the ceiling the path kernel's
+ * node, triangle and attribute fetches run against; no reference
+ * counterpart): raw buffer loads of width_bytes (4, 8, 12 or 16) per lane
+ * from a 1 MiB L2-resident table, 4 independent chains per lane, 8 waves per
+ * SIMD on every CU, the 64 lanes of a wave reading `distinct` addresses
+ * (1: one per wave-instruction ... 64: one per lane).  *lane_loads_per_s =
+ * lane loads (one per active lane per instruction) per second, best of 3
+ * warm launches.  Synchronous; a few ms. */
+int vrhip_microbench_vmem(int device, uint32_t width_bytes, uint32_t distinct, double *lane_loads_per_s);
 /* Raw debug slots: [0..7] the last counted render's counters; [8..13] phase
  * cycle totals (spheres, mesh traversal, hit materialisation, shading,
  * tonemap, whole kernel) written only by a -DVR_TIMING diagnostic build. */

@@ -69,3 +69,21 @@ def test_tile_sharded_render_equals_single_process(oracle, world):
     sc = scenes.make_scene("C2", 64, 112)
     ref, _, _, _ = po.render(sc, frames=4, times=[12345 + f for f in range(1, 5)])
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no external launcher starts two ranks
+    (torch.distributed.run as a child process) that form one process group;
+    --check-launch stops before any GPU work, so this runs on CPU."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    res = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--check-launch"],
+                         cwd=repo, env=env, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, res.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["gpus_arg"] == 2

@@ -74,14 +74,16 @@ def test_tile_gather_equals_single_rank(native, world):
 
 
 def test_bench_two_ranks_gloo_rehearsal(native):
-    env = dict(os.environ, VRHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--frames-per-step", "2", "--no-cpu"]
+    """`python bench.py --gpus 2` with no external launcher: bench.py starts
+    the two ranks itself (they share cuda:0 over gloo here)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(VRHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--frames-per-step", "2", "--no-cpu", "--no-roof", "--interactive-frames", "2"]
     res = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, res.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["scaling"] == "strong"
-    assert out["config"]["parallelism"] == "tile2"
+    assert out["config"]["parallelism"] == "tile2" and out["interactive"]["frames_per_step"] == 1

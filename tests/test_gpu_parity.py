@@ -17,7 +17,7 @@ from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math, selfte
 
 pytestmark = pytest.mark.gpu
 
-TOL_RMSE = {"hdri": 1e-3, "cornell": 2e-2}
+TOL_RMSE = 1e-3          # north_star: per-pixel RMSE < 1e-3 vs the reference at equal spp
 TOL_PIX_FRAC = 0.99
 
 
@@ -135,20 +135,111 @@ def test_render_bitexact_vs_portable_oracle(native, oracle, cfg, w, h, frames):
     assert_bitexact(gd, od, sc, "depth8")
 
 
-@pytest.mark.parametrize("cfg,w,h,frames,kind", [
-    ("C1", 128, 128, 4, "cornell"),
-    ("C3", 160, 96, 4, "hdri"),
+@pytest.mark.parametrize("cfg,w,h,frames", [
+    ("C1", 128, 128, 8),
+    ("C2", 160, 96, 8),
+    ("C3", 160, 96, 8),
+    ("C4", 144, 96, 8),
+    ("C5", 96, 64, 8),      # the 1M-triangle knot (depth-22 tree, 24-entry-stack kernels)
 ])
-def test_render_tolerance_vs_glibc_oracle(native, oracle, cfg, w, h, frames, kind):
+def test_render_tolerance_vs_glibc_oracle(native, oracle, cfg, w, h, frames):
+    """Default (t-culled) GPU render vs the oracle with glibc's libm -- the
+    semantics of the survey's probe of the reference -- at equal spp: image
+    RMSE of accum/frames below the north-star 1e-3 and >= 99 % of pixels with
+    max-channel |delta| <= 1e-3."""
     sc = scenes.make_scene(cfg, w, h)
-    ga, _, _, _ = gpu_render(sc, frames)
-    oa, _, _, _ = po.render(sc, frames=frames, libm=po.LIBM_GLIBC)
+    times = [sc["time"] + 11 * i for i in range(frames)]
+    ga, _, _, _ = gpu_render(sc, frames, times)
+    oa, _, _, _ = po.render(sc, frames=frames, times=times, libm=po.LIBM_GLIBC)
     g = rendered(ga, sc)[..., :3] / frames
     o = rendered(oa, sc)[..., :3] / frames
     d = np.abs(g - o).max(-1)
     rmse = float(np.sqrt(((g - o) ** 2).mean()))
-    assert rmse < TOL_RMSE[kind], rmse
-    assert (d <= 1e-3).mean() >= TOL_PIX_FRAC, (d <= 1e-3).mean()
+    frac = float((d <= 1e-3).mean())
+    print(f"{cfg} {w}x{h} {frames} frames vs glibc oracle: RMSE {rmse:.3e}, {frac:.5f} of pixels within 1e-3")
+    assert rmse < TOL_RMSE, rmse
+    assert frac >= TOL_PIX_FRAC, frac
+
+
+@pytest.mark.parametrize("cfg,w,h", [("C5", 96, 64), ("C5", 64, 48)])
+def test_c5_tree_bitexact_vs_portable_oracle(native, oracle, cfg, w, h):
+    """C5's 1M-triangle knot (depth-22 SBVH-class tree, the 24-entry-stack
+    kernels the 4K bench runs): strict traversal bit-exact against the
+    oracle (accum, RGBA8, depth), the default t-culled traversal too."""
+    sc = scenes.make_scene(cfg, w, h)
+    times = [sc["time"], sc["time"] + 1, sc["time"] + 2]
+    oa, orgba, od, _ = po.render(sc, frames=3, times=times, libm=po.LIBM_PORTABLE)
+    sa, srgba, sd, _ = gpu_render(sc, 3, times, strict=True)
+    assert_bitexact(sa, oa, sc, "accum (strict)")
+    assert_bitexact(srgba, orgba, sc, "rgba8 (strict)")
+    assert_bitexact(sd, od, sc, "depth8 (strict)")
+    ca, crgba, _, _ = gpu_render(sc, 3, times)
+    assert_bitexact(ca, oa, sc, "accum (culled)")
+    assert_bitexact(crgba, orgba, sc, "rgba8 (culled)")
+
+
+@pytest.mark.parametrize("cfg,w,h,frames", [("C2", 160, 96, 3), ("C3", 160, 96, 2), ("C4", 144, 96, 2),
+                                            ("C5", 96, 64, 2), ("C1", 96, 96, 3)])
+def test_profiled_render_is_the_production_render(native, cfg, w, h, frames):
+    """vrhip_render_profiled (the instrumented copy of the production kernels
+    that the roofline's executed bytes come from) renders the same bits as
+    vrhip_render, and its counts are consistent with the reference-algorithm
+    counts: the same rays, no more node visits or triangle tests."""
+    sc = scenes.make_scene(cfg, w, h)
+    times = [sc["time"] + i for i in range(frames)]
+    base = gpu_render(sc, frames, times)
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    e = r.render_profiled(frames=frames, times=times)
+    got = r.read_accum(), r.read_rgba8(), r.read_depth8()
+    r.set_strict_traversal(True)
+    r.clearBuffer()
+    ref = r.render_counted(frames=frames, times=times)
+    r.cleanUp()
+    for g, b, what in zip(got, base, ("accum", "rgba8", "depth8")):
+        assert_bitexact(g, b, sc, what)
+    assert e["node_visits_lds"] <= e["node_visits"] <= ref["node_visits"]
+    assert e["tri_tests"] <= ref["tri_tests"] and e["tri_loads"] >= e["tri_tests"]
+    assert e["nmap_hits"] <= e["mesh_hits"]
+    assert e["hdr_fetches"] == ref["hdr_fetches"] and e["brdf_fetches"] <= ref["brdf_fetches"]
+    if sc.get("mesh_flat") is None:
+        assert e["node_visits"] == 0 and e["mesh_hits"] == 0
+    else:
+        assert e["mesh_hits"] > 0 and e["tri_loads"] > 0
+
+
+def test_vmem_roof_microbench(native):
+    """The live gather-roof micro-benchmark (vrhip_microbench_vmem) runs and
+    reports finite, ordered rates for every load width."""
+    from vrenderer_pathtracer_amd import microbench_vmem
+    for w in (16, 12, 8, 4):
+        rates = [microbench_vmem(w, d) for d in (1, 64)]
+        print(f"b{8 * w}: {rates[0] / 1e9:.1f} / {rates[1] / 1e9:.1f} G lane-loads/s (1 / 64 addresses per instruction)")
+        assert all(1e9 < x < 1e14 for x in rates)
+
+
+def test_comm_gather_single_rank_through_c_abi(native):
+    """vrhip_comm_unique_id / _init / _gather / _destroy (RCCL ncclGather) on a
+    one-rank communicator: the gathered RGBA8 and accumulation equal the plain
+    render (RCCL refuses two ranks on one GPU; the 8-GPU path runs in the
+    driver's scaling bench, the multi-rank logic in the gloo tests)."""
+    from vrenderer_pathtracer_amd.renderer import comm_unique_id
+    from vrenderer_pathtracer_amd.tiles import WHAT_ACCUM, WHAT_RGBA8
+    sc = scenes.make_scene("C2", 160, 96)
+    times = [sc["time"], sc["time"] + 1]
+    base = gpu_render(sc, 2, times)
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.comm_init(0, 1, comm_unique_id())
+    r.render(frames=2, times=times, sync=False)
+    r.comm_gather(WHAT_RGBA8)
+    r.comm_gather(WHAT_ACCUM)
+    r.sync()
+    acc, rgba = r.read_accum(), r.read_rgba8()
+    r.comm_destroy()
+    r.cleanUp()
+    assert_bitexact(acc, base[0], sc, "accum")
+    assert_bitexact(rgba, base[1], sc, "rgba8")
 
 
 def test_grid_truncation_untouched_rows(native, oracle):

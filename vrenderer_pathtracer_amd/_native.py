@@ -28,7 +28,8 @@ _ctx = ctypes.c_void_p
 
 VRHIP_OK = 0
 ERRORS = {-1: "VRHIP_ERR_INVALID", -2: "VRHIP_ERR_HIP", -3: "VRHIP_ERR_NO_ENV", -4: "VRHIP_ERR_BVH",
-          -5: "VRHIP_ERR_NO_DEVICE", -6: "VRHIP_ERR_NOMEM"}
+          -5: "VRHIP_ERR_NO_DEVICE", -6: "VRHIP_ERR_NOMEM",
+          -7: "VRHIP_ERR_COMM"}
 
 _SIGNATURES = {
     "vrhip_last_error": (ctypes.c_char_p, []),
@@ -59,6 +60,10 @@ _SIGNATURES = {
     "vrhip_render": (ctypes.c_int, [_ctx, ctypes.c_uint32, _u32, ctypes.c_uint32]),
     "vrhip_render_counted": (ctypes.c_int, [_ctx, ctypes.c_uint32, _u32, ctypes.c_uint32,
                                             ctypes.POINTER(ctypes.c_uint64)]),
+    "vrhip_render_profiled": (ctypes.c_int, [_ctx, ctypes.c_uint32, _u32, ctypes.c_uint32,
+                                             ctypes.POINTER(ctypes.c_uint64)]),
+    "vrhip_microbench_vmem": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.POINTER(ctypes.c_double)]),
     "vrhip_kernel_stats": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.c_int]),
     "vrhip_debug_counters": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
@@ -76,6 +81,10 @@ _SIGNATURES = {
                                          _u32]),
     "vrhip_pack_tiles": (ctypes.c_int, [_ctx, ctypes.c_int, _vp]),
     "vrhip_unpack_tiles": (ctypes.c_int, [_ctx, ctypes.c_int, _vp, ctypes.c_uint32, ctypes.c_size_t]),
+    "vrhip_comm_unique_id": (ctypes.c_int, [_u8]),
+    "vrhip_comm_init": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32, _u8]),
+    "vrhip_comm_gather": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "vrhip_comm_destroy": (ctypes.c_int, [_ctx]),
     "vrhip_last_kernel_ms": (ctypes.c_int, [_ctx, _f]),
     "vrhip_bvh_info": (ctypes.c_int, [_ctx, _u32, _u32, _u32]),
     "vrhip_selftest_math": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _f, _f, _f, ctypes.c_size_t]),

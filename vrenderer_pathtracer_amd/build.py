@@ -52,7 +52,7 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None) -> str:
         return LIB_PATH
     tmp = LIB_PATH + ".tmp"
     cmd = [_hipcc()] + HIPCC_FLAGS + list(extra_flags or []) + ["-o", tmp] + \
-          [os.path.join(CSRC, s) for s in SOURCES] + ["-lz"]
+          [os.path.join(CSRC, s) for s in SOURCES] + ["-lz", "-lrccl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     res = subprocess.run(cmd, capture_output=True, text=True)

@@ -23,12 +23,24 @@ enum Flags : uint32_t {
     F_TEX_SPEC = 1u << 7,    // kHasSpecularMap     (:27)
     F_STRICT = 1u << 8,      // visit every pierced box, as the reference (no t-culling)
     F_WIDE = 1u << 9,        // culled traversal over the 4-wide collapse of the tree (bvh4)
+    // compile-time only (never in RenderParams::flags): the instrumented copy
+    // of the production kernels (vrhip_render_profiled) -- same algorithm,
+    // launch shape and results, plus per-lane counts of the memory operations
+    // they execute
+    F_COUNT_EXEC = 1u << 10,
 };
 
 constexpr int kMaxFramesPerLaunch = 64;
-// counting variant: rays, node visits, vert0 slot reads, triangle tests,
-// attribute bytes, texture fetches, HDRI fetches, BRDF lookups
+// counting variants, slots [0, kCounters): rays, node visits, vert0 slot
+// reads, triangle tests, attribute bytes, texture fetches, HDRI fetches, BRDF
+// lookups.  The instrumented production kernels also fill slots
+// [kExecCounterBase, +kExecCounters): node visits served from the LDS copy,
+// triangle loads issued (36 B each), mesh hits shaded, mesh hits shaded
+// through the normal map.  Slots 8..13 hold diagnostic-build phase timers.
 constexpr int kCounters = 8;
+constexpr int kExecCounterBase = 16;
+constexpr int kExecCounters = 4;
+constexpr int kWaveTimesBase = 32;   // -DVR_WAVE_TIMES diagnostic builds: per-wave records from here
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
 // render_wave_kernel work queues: RenderParams::n_queues counters (a power of
@@ -88,12 +100,16 @@ struct RenderParams {
 };
 
 // host-side launchers implemented in vr_kernel.hip
-int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, bool count, void* stream);
+// count: 0 production kernels, 1 reference-algorithm counting variant,
+// 2 instrumented production kernels (F_COUNT_EXEC)
+int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int count, void* stream);
 // use_scratch launches: sums the per-path results of launch_render in path order
 int launch_finish(const RenderParams& p, uint32_t n_tiles, void* stream);
 int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);
 int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,
                       uint32_t n_owned, uint32_t rank, uint32_t nranks, int unpack, void* stream);
+int launch_vmem_roof(int width, const uint32_t* tab, uint32_t n_lines, uint32_t distinct, int iters,
+                     uint32_t blocks, uint32_t* out, void* stream);
 int launch_selftest_math(int fn, const float* a, const float* b, float* out, size_t n, void* stream);
 int launch_selftest_exact(int fn, uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad,
                           void* stream);

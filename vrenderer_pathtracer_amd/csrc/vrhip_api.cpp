@@ -8,6 +8,7 @@
 // (cuda/src/PathTracer.cu:976-1001), and multi-frame render steps.
 #include <hip/hip_runtime.h>
 #include <hip/hip_gl_interop.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -114,6 +115,11 @@ struct vrhip_ctx {
     unsigned long long* counters = nullptr;
     // GL interop (colour, depth textures registered by the display host)
     hipGraphicsResource_t gl_res[2] = { nullptr, nullptr };
+    // multi-GPU tile gather (vrhip_comm_*): one RCCL communicator per context
+    ncclComm_t comm = nullptr;
+    uint8_t* comm_send = nullptr;    // this rank's packed tiles (largest element, 16 B/pixel)
+    uint8_t* comm_recv = nullptr;    // rank 0: n_ranks packed buffers, comm_slot bytes apart
+    size_t comm_slot = 0;            // bytes per rank slot (max owned pixels x 16 B)
 };
 
 namespace {
@@ -530,6 +536,8 @@ int vrhip_destroy(vrhip_ctx* c)
     for (int i = 0; i < 2; ++i)
         if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
     dfree(c->counters);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    dfree(c->comm_send); dfree(c->comm_recv);
     for (auto& l : c->lane) {
         dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr);
         if (l.done) (void)hipEventDestroy(l.done);
@@ -751,9 +759,9 @@ int vrhip_gl_present(vrhip_ctx* c)
 }
 
 #ifdef VR_WAVE_TIMES
-constexpr int kDebugSlots = 16 + 3 * 8192;   // + per-wave start / end / paths of render_wave_kernel
+constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192;   // + per-wave start / end / paths of render_wave_kernel
 #else
-constexpr int kDebugSlots = 16;
+constexpr int kDebugSlots = vr::kWaveTimesBase;
 #endif
 
 static int ensure_counters(vrhip_ctx* c)
@@ -845,7 +853,9 @@ static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t p
     return VRHIP_OK;
 }
 
-static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed, bool count)
+// count: 0 production, 1 reference-algorithm counting variant (in place, no
+// scratch), 2 instrumented production kernels (same launch shape as 0)
+static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed, int count)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     if (n_frames == 0) return VRHIP_OK;
@@ -891,7 +901,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
                                        : (c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 23 ? 24 : c->bvh_depth <= 30 ? 32 : 64);
     if (count) {
         if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
-        HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * vr::kCounters, c->stream));
+        HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kDebugSlots, c->stream));
         p.counters = c->counters;
     }
 #if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS) || defined(VR_WAVE_TIMES)
@@ -900,9 +910,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
 #endif
     if ((rc = account_pending(c, false)) != VRHIP_OK) return rc;
     const uint32_t k_max = std::min<uint32_t>(n_frames, (uint32_t)vr::kMaxFramesPerLaunch);
-    const uint32_t split_max = count ? 1u : choose_split(c, n_tiles, k_max);
+    const uint32_t split_max = count == 1 ? 1u : choose_split(c, n_tiles, k_max);
     p.path_stride = n_tiles * (uint32_t)vr::kBlockThreads;
-    p.use_scratch = count ? 0u : 1u;   // the counting variant accumulates in place
+    p.use_scratch = count == 1 ? 0u : 1u;   // the reference counting variant accumulates in place
     const size_t need = (size_t)2 * k_max * p.path_stride;   // scratch float4s of the largest launch
     if (p.use_scratch) {
         // the path-pool kernel is persistent: one resident set of blocks per
@@ -975,20 +985,72 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
 
 int vrhip_render(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed)
 {
-    return render_impl(c, n_frames, times, time_seed, false);
+    return render_impl(c, n_frames, times, time_seed, 0);
 }
 
 int vrhip_render_counted(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed,
                          uint64_t counters[8])
 {
     if (!counters) return fail(VRHIP_ERR_INVALID, "counters is NULL");
-    int rc = render_impl(c, n_frames, times, time_seed, true);
+    int rc = render_impl(c, n_frames, times, time_seed, 1);
     if (rc) return rc;
     unsigned long long h[vr::kCounters] = {};
     HIP_TRY(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int i = 0; i < vr::kCounters; ++i) counters[i] = (uint64_t)h[i];
     return VRHIP_OK;
+}
+
+int vrhip_render_profiled(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed,
+                          uint64_t counters[VRHIP_PROFILE_COUNTERS])
+{
+    if (!counters) return fail(VRHIP_ERR_INVALID, "counters is NULL");
+    static_assert(VRHIP_PROFILE_COUNTERS == vr::kCounters + vr::kExecCounters, "profile counter layout");
+    int rc = render_impl(c, n_frames, times, time_seed, 2);
+    if (rc) return rc;
+    unsigned long long h[vr::kExecCounterBase + vr::kExecCounters] = {};
+    HIP_TRY(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < vr::kCounters; ++i) counters[i] = (uint64_t)h[i];
+    for (int i = 0; i < vr::kExecCounters; ++i) counters[vr::kCounters + i] = (uint64_t)h[vr::kExecCounterBase + i];
+    return VRHIP_OK;
+}
+
+int vrhip_microbench_vmem(int device, uint32_t width_bytes, uint32_t distinct, double* lane_loads_per_s)
+{
+    if (!lane_loads_per_s || distinct == 0 || distinct > 64 || (64 % distinct) != 0 ||
+        (width_bytes != 4 && width_bytes != 8 && width_bytes != 12 && width_bytes != 16))
+        return fail(VRHIP_ERR_INVALID, "width must be 4/8/12/16 bytes, distinct a divisor of 64");
+    HIP_TRY(hipSetDevice(device));
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    const uint32_t n_lines = 1u << 14;                   // 1 MiB: L2-resident (4 MiB per XCD)
+    const uint32_t blocks = (uint32_t)cus * 8u;          // 8 waves per SIMD
+    const int iters = 256;
+    uint32_t* tab = nullptr;
+    HIP_TRY(hipMalloc((void**)&tab, (size_t)n_lines * 64 + 64));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    auto done = [&](int code) {
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        (void)hipFree(tab);
+        return code;
+    };
+    if (hipMemset(tab, 0, (size_t)n_lines * 64 + 64) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess)
+        return done(fail(VRHIP_ERR_HIP, "microbench setup failed"));
+    float best = 1e30f;
+    for (int rep = 0; rep < 4; ++rep) {                  // the first launch warms the caches
+        if (hipEventRecord(e0, nullptr) != hipSuccess ||
+            vr::launch_vmem_roof((int)width_bytes, tab, n_lines, distinct, iters, blocks, tab + n_lines * 16, nullptr) != 0 ||
+            hipEventRecord(e1, nullptr) != hipSuccess || hipEventSynchronize(e1) != hipSuccess)
+            return done(fail(VRHIP_ERR_HIP, "microbench launch failed"));
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (rep > 0 && ms < best) best = ms;
+    }
+    *lane_loads_per_s = (double)blocks * 256.0 * iters * 4.0 / (best * 1e-3);
+    return done(VRHIP_OK);
 }
 
 int vrhip_debug_counters(vrhip_ctx* c, uint64_t out[16], int reset)
@@ -1135,6 +1197,76 @@ int vrhip_unpack_tiles(vrhip_ctx* c, int what, const void* src, uint32_t n_ranks
         if (e) return fail(VRHIP_ERR_HIP, "unpack launch failed");
         s += stride_bytes ? stride_bytes : (size_t)n_owned * 256u * elem_size(what);
     }
+    return VRHIP_OK;
+}
+
+// ---- multi-GPU tile gather over RCCL ------------------------
+static int nccl_fail(ncclResult_t r, const char* what)
+{
+    return fail(VRHIP_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+static uint32_t max_owned_pixels(uint32_t W, uint32_t H, uint32_t n_ranks)
+{
+    return owned_tiles_of(W, H, 0, n_ranks) * 256u;       // rank 0 owns the most tiles
+}
+
+int vrhip_comm_unique_id(uint8_t id[VRHIP_COMM_ID_BYTES])
+{
+    if (!id) return fail(VRHIP_ERR_INVALID, "id is NULL");
+    static_assert(VRHIP_COMM_ID_BYTES == sizeof(ncclUniqueId), "ncclUniqueId size");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGetUniqueId");
+    std::memcpy(id, &u, sizeof(u));
+    return VRHIP_OK;
+}
+
+int vrhip_comm_init(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks, const uint8_t id[VRHIP_COMM_ID_BYTES])
+{
+    if (!c || !id || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad communicator arguments");
+    int rc = set_device(c); if (rc) return rc;
+    if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
+    dfree(c->comm_send); dfree(c->comm_recv);
+    if ((rc = vrhip_set_tiling(c, rank, n_ranks)) != VRHIP_OK) return rc;
+    c->comm_slot = (size_t)max_owned_pixels(c->W, c->H, n_ranks) * 16u;
+    const size_t slot = c->comm_slot ? c->comm_slot : 16u;
+    if (hipMalloc((void**)&c->comm_send, slot) != hipSuccess ||
+        (rank == 0 && hipMalloc((void**)&c->comm_recv, slot * n_ranks) != hipSuccess))
+        return fail(VRHIP_ERR_NOMEM, "gather buffers");
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    const ncclResult_t r = ncclCommInitRank(&c->comm, (int)n_ranks, u, (int)rank);   // blocks until every rank joins
+    if (r != ncclSuccess) { c->comm = nullptr; return nccl_fail(r, "ncclCommInitRank"); }
+    return VRHIP_OK;
+}
+
+int vrhip_comm_gather(vrhip_ctx* c, int what)
+{
+    if (!c || what < 0 || what > 2) return fail(VRHIP_ERR_INVALID, "bad gather arguments");
+    if (!c->comm) return fail(VRHIP_ERR_INVALID, "vrhip_comm_init has not been called");
+    int rc = set_device(c); if (rc) return rc;
+    // pack -> gather -> (rank 0) unpack, all on the context stream, behind the
+    // finish passes that wrote the images
+    const size_t bytes = (size_t)max_owned_pixels(c->W, c->H, c->nranks) * (size_t)elem_size(what);
+    if ((rc = vrhip_pack_tiles(c, what, c->comm_send)) != VRHIP_OK) return rc;
+    const ncclResult_t r = ncclGather(c->comm_send, c->comm_recv, bytes, ncclUint8, 0, c->comm, c->stream);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGather");
+    if (c->rank == 0) return vrhip_unpack_tiles(c, what, c->comm_recv, c->nranks, bytes);
+    return VRHIP_OK;
+}
+
+int vrhip_comm_destroy(vrhip_ctx* c)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    int rc = set_device(c); if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->comm) {
+        const ncclResult_t r = ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+        if (r != ncclSuccess) return nccl_fail(r, "ncclCommDestroy");
+    }
+    dfree(c->comm_send); dfree(c->comm_recv);
     return VRHIP_OK;
 }
 

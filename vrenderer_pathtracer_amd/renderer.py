@@ -328,6 +328,22 @@ class VRendererHIP:
         check(self._lib.vrhip_unpack_tiles(self._need_ctx(), what, ctypes.c_void_p(src_ptr), n_ranks, stride_bytes),
               "vrhip_unpack_tiles")
 
+    # -- multi-GPU tile gather over RCCL (vrhip_comm_*) --------------------
+    def comm_init(self, rank: int, n_ranks: int, unique_id: bytes) -> None:
+        """Join the n_ranks RCCL communicator named by unique_id (from
+        comm_unique_id() on rank 0) and take tiles rank, rank+n, ... ."""
+        if len(unique_id) != COMM_ID_BYTES:
+            raise ValueError(f"unique id must be {COMM_ID_BYTES} bytes")
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(unique_id)
+        check(self._lib.vrhip_comm_init(self._need_ctx(), rank, n_ranks, buf), "vrhip_comm_init")
+
+    def comm_gather(self, what: int) -> None:
+        """Pack, ncclGather to rank 0, unpack on rank 0 (enqueued on the context stream)."""
+        check(self._lib.vrhip_comm_gather(self._need_ctx(), int(what)), "vrhip_comm_gather")
+
+    def comm_destroy(self) -> None:
+        check(self._lib.vrhip_comm_destroy(self._need_ctx()), "vrhip_comm_destroy")
+
     def render_counted(self, frames: int = 1, times=None, time_seed=None) -> dict:
         """Render through the counting kernel variant; returns the event counts."""
         arr = None
@@ -340,6 +356,21 @@ class VRendererHIP:
               "vrhip_render_counted")
         names = ["rays", "node_visits", "slot_reads", "tri_tests", "attr_bytes", "tex_fetches", "hdr_fetches",
                  "brdf_fetches"]
+        return {n: int(v) for n, v in zip(names, c)}
+
+    def render_profiled(self, frames: int = 1, times=None, time_seed=None) -> dict:
+        """Render through the instrumented production kernels (vrhip_render_profiled):
+        the same work as render(), plus counts of the memory operations it issues."""
+        arr = None
+        if times is not None:
+            arr = (ctypes.c_uint32 * frames)(*[int(t) & 0xFFFFFFFF for t in times])
+        if time_seed is None:
+            time_seed = self.default_time if self.default_time is not None else int(_time.time() * 1000)
+        c = (ctypes.c_uint64 * 12)()
+        check(self._lib.vrhip_render_profiled(self._need_ctx(), frames, arr, int(time_seed) & 0xFFFFFFFF, c),
+              "vrhip_render_profiled")
+        names = ["rays", "node_visits", "slot_reads", "tri_tests", "attr_bytes", "tex_fetches", "hdr_fetches",
+                 "brdf_fetches", "node_visits_lds", "tri_loads", "mesh_hits", "nmap_hits"]
         return {n: int(v) for n, v in zip(names, c)}
 
     def kernel_stats(self, reset: bool = False):
@@ -405,6 +436,23 @@ def selftest_sqrt(lo_bits: int, hi_bits: int, device: int = 0):
     check(_native.lib().vrhip_selftest_sqrt(device, lo_bits, hi_bits, ctypes.byref(n), ctypes.byref(first)),
           "vrhip_selftest_sqrt")
     return int(n.value), int(first.value)
+
+
+def microbench_vmem(width_bytes: int, distinct: int, device: int = 0) -> float:
+    """Lane loads per second of the device's vector-memory gather path (vrhip_microbench_vmem)."""
+    r = ctypes.c_double(0)
+    check(_native.lib().vrhip_microbench_vmem(device, width_bytes, distinct, ctypes.byref(r)), "vrhip_microbench_vmem")
+    return float(r.value)
+
+
+COMM_ID_BYTES = 128    # VRHIP_COMM_ID_BYTES
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL communicator id (vrhip_comm_unique_id), to hand to every rank."""
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    check(_native.lib().vrhip_comm_unique_id(buf), "vrhip_comm_unique_id")
+    return bytes(buf)
 
 
 def device_count() -> int:

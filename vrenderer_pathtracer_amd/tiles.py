@@ -8,8 +8,9 @@ ranks in row-major tile order, so ranks own equal tile counts (+-1) spread
 over the whole image (sky vs mesh load balance).  Each rank keeps its own
 float4 accumulation resident; after every accumulation step the ranks' RGBA8
 tiles (or float4 accumulation, for parity read-out) are gathered to rank 0
-with ONE collective (torch.distributed "nccl" = RCCL over xGMI, or gloo on
-CPU) and scattered back into image order on the device.
+with ONE collective (ncclGather over xGMI inside libvrhip.so,
+vrhip_comm_gather; gloo through host memory for one-GPU rehearsals) and
+scattered back into image order on the device.
 """
 from __future__ import annotations
 
@@ -63,45 +64,60 @@ def unpack_host(packed: list, out: np.ndarray) -> np.ndarray:
 class TileGather:
     """Per-step gather of every rank's tiles to rank 0 with one collective.
 
-    renderer: VRendererHIP with set_tiling(rank, world) applied; torch tensors
-    hold the send/receive buffers on the renderer's device so the collective
-    runs over RCCL (backend "nccl"); rank 0's renderer receives the full
-    image.  With the gloo backend (CPU rehearsal of the multi-rank path on one
-    GPU) the buffers are staged through host memory.
+    backend "nccl" (the measured configuration, one rank per GPU): the
+    library's own RCCL communicator -- rank 0 draws the id
+    (vrhip_comm_unique_id), torch.distributed only hands it to the other
+    ranks, and every step is vrhip_comm_gather (pack, ncclGather, unpack on
+    rank 0, enqueued on the renderer's stream).  backend "gloo" (a CPU/one-GPU
+    rehearsal of the multi-rank path with several ranks sharing a device,
+    which RCCL refuses): packed buffers staged through host memory and
+    gathered by torch.distributed.
     """
 
     def __init__(self, renderer, rank: int, world: int, device, what: int = WHAT_RGBA8):
-        import torch
-        import torch.distributed as dist
         self.r, self.rank, self.world, self.what = renderer, rank, world, what
         self.device = device
+        self.native = False
+        if world == 1:
+            return
+        import torch
+        import torch.distributed as dist
+        if dist.get_backend() != "gloo":
+            from .renderer import COMM_ID_BYTES, comm_unique_id
+            uid = torch.zeros(COMM_ID_BYTES, dtype=torch.uint8, device=device)
+            if rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
+            dist.broadcast(uid, src=0)
+            renderer.comm_init(rank, world, bytes(uid.cpu().numpy().tobytes()))
+            self.native = True
+            return
         H, W = renderer.height, renderer.width
         self.stride = max_owned_pixels(W, H, world) * _ELEM_BYTES[what]
         self.send = torch.empty(self.stride, dtype=torch.uint8, device=device)
         self.recv = None
-        self.host = world > 1 and dist.get_backend() == "gloo"
-        if rank == 0 and world > 1:
+        if rank == 0:
             self.recv = torch.empty(world * self.stride, dtype=torch.uint8, device=device)
-            views = self.recv.cpu() if self.host else self.recv
-            self.recv_stage = views
-            self.views = list(views.view(world, self.stride).unbind(0))
+            self.recv_stage = self.recv.cpu()
+            self.views = list(self.recv_stage.view(world, self.stride).unbind(0))
 
     def step(self) -> None:
-        import torch
-        import torch.distributed as dist
         if self.world == 1:
             return
-        own_stream = self.r.get_stream() != torch.cuda.current_stream(self.device).cuda_stream
-        if own_stream:
-            torch.cuda.current_stream(self.device).synchronize()   # the last collective has read `send`
+        if self.native:
+            self.r.comm_gather(self.what)
+            return
+        import torch
+        import torch.distributed as dist
+        torch.cuda.current_stream(self.device).synchronize()
         self.r.pack_tiles(self.what, self.send.data_ptr())
-        if own_stream or self.host:
-            self.r.sync()                     # the collective reads `send` on torch's stream
-        send = self.send.cpu() if self.host else self.send
-        dist.gather(send, self.views if self.rank == 0 else None, dst=0)
+        self.r.sync()                          # the packed tiles are complete before the host copy
+        dist.gather(self.send.cpu(), self.views if self.rank == 0 else None, dst=0)
         if self.rank == 0:
-            if self.host:
-                self.recv.copy_(self.recv_stage)
-            if own_stream or self.host:
-                torch.cuda.current_stream(self.device).synchronize()
+            self.recv.copy_(self.recv_stage)
+            torch.cuda.current_stream(self.device).synchronize()
             self.r.unpack_tiles(self.what, self.recv.data_ptr(), self.world, self.stride)
+
+    def close(self) -> None:
+        if self.native:
+            self.r.comm_destroy()
+            self.native = False
