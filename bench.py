@@ -354,7 +354,7 @@ def main():
         ref_b = reference_bytes(ref_counts, own_paths, owned * F)
         achieved = load_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         roofs = {}
-        if roof:
+        if roof and load_bytes > 0:
             t_min = sum(n / roof[w]["best"] for w, n in loads.items())
             roofs["vmem"] = {"achieved": round(achieved, 1), "peak": round(load_bytes / t_min / 1e9, 1),
                              "frac": round(t_min / avg_launch_s, 4)}

@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <iostream>
 
 vRendererHIP::vRendererHIP() :
@@ -151,12 +152,98 @@ void vRendererHIP::cleanUp()
   }
 }
 
+// The device layout of src/vRendererCuda.cpp:204-279, built from the
+// application's own SBVH: node = 4 float4 (child 0 x/y bounds, child 1 x/y
+// bounds, both z bounds, child indices); a child index >= 0 is the float4
+// offset of an inner node, < 0 the complement of the child leaf's first
+// triangle slot; a leaf's triangles take 3 consecutive slots each (vertices,
+// normals, tangents as float4, uvs as float2) in SBVH triangle-reference order
+// and end with a 0x80000000 terminator slot.  Nodes are laid out in the order
+// a LIFO walk from the root reaches them (children taken in order, so the
+// second child's subtree is emitted first), as the CUDA backend does; the
+// library keeps the tree's child order and leaf triangle order, hence the
+// reference's visit order and equal-t tie resolution.
+bool vRendererHIP::flattenSBVH(const vMeshData &_meshData, FlatMesh &_out)
+{
+  _out = FlatMesh();
+  const BVHNode *root = _meshData.m_bvh.getRoot();
+  if(!root || root->isLeaf())
+    return false;
+  auto bits = [](uint32_t _u) { float f; std::memcpy(&f, &_u, 4); return f; };
+  auto pushRow = [](std::vector<float> &_v, float _a, float _b, float _c, float _d) {
+    _v.push_back(_a); _v.push_back(_b); _v.push_back(_c); _v.push_back(_d);
+  };
+  struct Pending { const BVHNode *node; size_t row; };   // row = float4 offset of the node
+  std::vector<Pending> todo{ { root, 0 } };
+  _out.bvh.assign(16, 0.f);
+  while(!todo.empty())
+  {
+    const Pending cur = todo.back();
+    todo.pop_back();
+    AABB box[2];
+    int32_t link[2];
+    for(unsigned int c = 0; c < 2; ++c)
+    {
+      const BVHNode *child = cur.node->childNode(c);
+      box[c] = child->getBounds();
+      if(!child->isLeaf())
+      {
+        link[c] = static_cast<int32_t>(_out.bvh.size() / 4);
+        todo.push_back({ child, _out.bvh.size() / 4 });
+        _out.bvh.resize(_out.bvh.size() + 16, 0.f);
+        continue;
+      }
+      const LeafNode *leaf = static_cast<const LeafNode *>(child);
+      link[c] = ~static_cast<int32_t>(_out.verts.size() / 4);
+      for(unsigned int j = leaf->firstIndex(); j < leaf->lastIndex(); ++j)
+      {
+        const vHTriangle &tri = _meshData.m_triangles[_meshData.m_bvh.getTriIndex(j)];
+        for(unsigned int k = 0; k < 3; ++k)
+        {
+          const vHVert &v = _meshData.m_vertices[tri.m_indices[k]];
+          pushRow(_out.verts, v.m_vert.m_x, v.m_vert.m_y, v.m_vert.m_z, 0.f);
+          pushRow(_out.normals, v.m_normal.m_x, v.m_normal.m_y, v.m_normal.m_z, 0.f);
+          pushRow(_out.tangents, v.m_tangent.m_x, v.m_tangent.m_y, v.m_tangent.m_z, 0.f);
+          _out.uvs.push_back(v.m_u);
+          _out.uvs.push_back(v.m_v);
+        }
+      }
+      pushRow(_out.verts, bits(0x80000000u), 0.f, 0.f, 0.f);
+      pushRow(_out.normals, bits(0x80000000u), 0.f, 0.f, 0.f);
+      pushRow(_out.tangents, bits(0x80000000u), 0.f, 0.f, 0.f);
+      _out.uvs.push_back(bits(0x80000000u));
+      _out.uvs.push_back(0.f);
+    }
+    float *n = &_out.bvh[4 * cur.row];
+    const ngl::Vec3 lo0 = box[0].minBounds(), hi0 = box[0].maxBounds();
+    const ngl::Vec3 lo1 = box[1].minBounds(), hi1 = box[1].maxBounds();
+    const float rows[16] = { lo0.m_x, hi0.m_x, lo0.m_y, hi0.m_y,
+                             lo1.m_x, hi1.m_x, lo1.m_y, hi1.m_y,
+                             lo0.m_z, hi0.m_z, lo1.m_z, hi1.m_z,
+                             bits(static_cast<uint32_t>(link[0])), bits(static_cast<uint32_t>(link[1])), 0.f, 0.f };
+    std::memcpy(n, rows, sizeof(rows));
+  }
+  return true;
+}
+
 void vRendererHIP::initMesh(const vMeshData &_meshData)
 {
-  // The closest hit does not depend on the tree (the reference traversal
-  // visits every pierced box, cuda/src/PathTracer.cu:316,322), so the
-  // library builds its own binned-SAH BVH from the indexed mesh instead of
-  // re-flattening the host SBVH (src/vRendererCuda.cpp:204-279).
+  // Default: upload the application's SBVH in the reference's flattened
+  // layout (the traversal then visits nodes and resolves equal-t ties exactly
+  // as the CUDA backend does).  VRHIP_NATIVE_BVH=1 instead rebuilds a binned-
+  // SAH tree from the indexed mesh in the library (same closest hits up to
+  // the order of exactly tied triangles; the SBVH build is then unnecessary).
+  const char *native = std::getenv("VRHIP_NATIVE_BVH");
+  if(!(native && native[0] == '1'))
+  {
+    FlatMesh flat;
+    if(!flattenSBVH(_meshData, flat))
+      validate(VRHIP_ERR_BVH, "Flatten SBVH (empty tree or a leaf root)");
+    validate(vrhip_upload_mesh_flat(m_ctx, flat.bvh.data(), flat.bvh.size() / 4, flat.verts.data(),
+                                    flat.normals.data(), flat.tangents.data(), flat.uvs.data(), flat.verts.size() / 4),
+             "Upload mesh");
+    return;
+  }
   const size_t nv = _meshData.m_vertices.size();
   std::vector<float> pos(3 * nv), nrm(3 * nv), tan(3 * nv), uv(2 * nv);
   for(size_t i = 0; i < nv; ++i)

@@ -39,6 +39,16 @@ public:
   bool loadBRDF(const float *_brdf) override;
   unsigned int getFrameCount() const override;
 
+  /// The reference's flattened mesh layout (src/vRendererCuda.cpp:204-279):
+  /// float4 rows for bvh/verts/normals/tangents, float2 for uvs.
+  struct FlatMesh
+  {
+    std::vector<float> bvh, verts, normals, tangents, uvs;
+  };
+  /// Flattens the application's SBVH (vMeshData::m_bvh) into that layout, as
+  /// initMesh uploads it; false for an empty tree or a leaf root.  Host only.
+  static bool flattenSBVH(const vMeshData &_meshData, FlatMesh &_out);
+
 private:
   /// Reference error behaviour (src/vRendererCuda.cpp:454-467): message,
   /// errorlog.txt, exit(0).  The C ABI itself only returns status codes.
