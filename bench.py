@@ -97,16 +97,17 @@ def reference_bytes(c: dict, paths: int, pixel_frames: int) -> float:
 
 def executed_loads(e: dict, paths: int, wave_kernel: bool) -> dict:
     """Per-lane global loads the production render kernels issue, by width
-    (bytes): node rows 3x16 + child indices 8 per node visit not served from
-    LDS; triangles 3x12 (v0, two edges) per triangle load; per mesh hit shaded
-    uv 3x8 + tangents 3x16 + normals 3x16 (normal map) or vertices 3x12 (face
+    (bytes): the node visits not served from LDS (counted by width in the
+    kernel: 2x16 per conservative fp16 node, 3x16 + 8 per fp32 node);
+    triangles 3x12 (v0, two edges) per triangle load; per mesh hit shaded uv
+    3x8 + tangents 3x16 + normals 3x16 (normal map) or vertices 3x12 (face
     normal); 16 per texture / HDRI texel; 3x4 per BRDF lookup; 2x16 primary
     record per path (path kernel)."""
-    glob = e["node_visits"] - e["node_visits_lds"]
     hits, nmap = e["mesh_hits"], e["nmap_hits"]
-    return {16: 3 * glob + 3 * hits + 3 * nmap + e["tex_fetches"] + e["hdr_fetches"] + (2 * paths if wave_kernel else 0),
+    return {16: e["node_lane_loads_b128"] + 3 * hits + 3 * nmap + e["tex_fetches"] + e["hdr_fetches"]
+            + (2 * paths if wave_kernel else 0),
             12: 3 * e["tri_loads"] + 3 * (hits - nmap),
-            8: glob + 3 * hits,
+            8: e["node_lane_loads_b64"] + 3 * hits,
             4: 3 * e["brdf_fetches"]}
 
 
@@ -349,7 +350,7 @@ def main():
         avg_launch_s = (kms / 1e3) / max(launches, 1)
         loads = executed_loads(exec_counts, own_paths, mesh)
         load_bytes = sum(w * n for w, n in loads.items())
-        lds_bytes = 56 * exec_counts["node_visits_lds"]
+        lds_bytes = (32 if exec_counts["node_lane_loads_b64"] == 0 else 56) * exec_counts["node_visits_lds"]
         store_bytes = 16 * own_paths + (32 * owned if mesh else 0)
         ref_b = reference_bytes(ref_counts, own_paths, owned * F)
         achieved = load_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
@@ -363,6 +364,11 @@ def main():
         if traffic and world == 1:
             hbm_gbs = traffic / avg_launch_s / 1e9
             roofs["hbm"] = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(hbm_gbs / HBM_PEAK_GBS, 4)}
+        if load_bytes == 0:
+            # sphere-only scenes (C1): no global loads on the path -- the
+            # kernel is VALU-bound (sphere tests, libm); report the HBM line only
+            roofs.pop("l2", None)
+            roofs.setdefault("hbm", {"achieved": 0.0, "peak": HBM_PEAK_GBS, "frac": 0.0})
         bound = max(roofs, key=lambda k: roofs[k]["frac"])
         roofline = {"bound": bound, "achieved": roofs[bound]["achieved"], "peak": roofs[bound]["peak"], "unit": "GB/s",
                     "frac": roofs[bound]["frac"], "traffic": traffic if world == 1 else None,

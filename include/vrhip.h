@@ -169,10 +169,12 @@ int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *time
  * counters[0..7] as vrhip_render_counted but for the executed work
  * (attribute bytes include the 36 B of vertices a mesh hit's face normal
  * reads), then [8] node visits served from the block's LDS copy of the tree
- * top (the rest read 3x16 B + 8 B from memory), [9] triangle loads issued
+ * top, [9] triangle loads issued
  * (36 B each; an odd leaf's last pair loads its triangle twice), [10] mesh
- * hits shaded, [11] of those through the normal map.  Synchronous. */
-#define VRHIP_PROFILE_COUNTERS 12
+ * hits shaded, [11] of those through the normal map, [12] / [13] 16-B / 8-B
+ * lane loads of the node visits served from memory (fp32 nodes: 3 + 1 per
+ * visit; the default conservative fp16 nodes: 2 + 0).  Synchronous. */
+#define VRHIP_PROFILE_COUNTERS 14
 int vrhip_render_profiled(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
                           uint64_t counters[VRHIP_PROFILE_COUNTERS]);
 int vrhip_sync(vrhip_ctx *ctx);

@@ -2,7 +2,9 @@
 // NGLScene does (src/NGLScene.cpp:82-89,196-197,224,259,443-456), with
 // stand-in Camera/GL implementations.  Writes the last RGBA8 image uploaded
 // to the colour texture and the frame count to argv[1].
+#include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -35,10 +37,116 @@ float Camera::getFovScale() const
   return std::tan(75.f * kDegInRad / 2.f);
 }
 
+// ---- a host SBVH for the mesh mode -----------------------------------------
+// The application hands initMesh a vMeshData whose m_bvh its SBVH builder
+// made (src/SBVH.cpp); this driver stands in with a median-split tree over
+// triangle centroids (leaves of <= 4 triangles) in the stand-in node classes.
+static AABB triBounds(const vMeshData &_m, const std::vector<unsigned int> &_ref, size_t _a, size_t _b)
+{
+  ngl::Vec3 lo, hi;
+  lo.m_x = lo.m_y = lo.m_z = 1e30f;
+  hi.m_x = hi.m_y = hi.m_z = -1e30f;
+  for(size_t i = _a; i < _b; ++i)
+    for(int k = 0; k < 3; ++k)
+    {
+      const ngl::Vec3 &v = _m.m_vertices[_m.m_triangles[_ref[i]].m_indices[k]].m_vert;
+      lo.m_x = std::fmin(lo.m_x, v.m_x); lo.m_y = std::fmin(lo.m_y, v.m_y); lo.m_z = std::fmin(lo.m_z, v.m_z);
+      hi.m_x = std::fmax(hi.m_x, v.m_x); hi.m_y = std::fmax(hi.m_y, v.m_y); hi.m_z = std::fmax(hi.m_z, v.m_z);
+    }
+  return AABB(lo, hi);
+}
+
+static BVHNode *buildTree(const vMeshData &_m, std::vector<unsigned int> &_ref, size_t _a, size_t _b)
+{
+  const AABB box = triBounds(_m, _ref, _a, _b);
+  if(_b - _a <= 4)
+    return new LeafNode(box, static_cast<unsigned int>(_a), static_cast<unsigned int>(_b));
+  const ngl::Vec3 lo = box.minBounds(), hi = box.maxBounds();
+  const float ext[3] = { hi.m_x - lo.m_x, hi.m_y - lo.m_y, hi.m_z - lo.m_z };
+  const int axis = ext[0] >= ext[1] && ext[0] >= ext[2] ? 0 : (ext[1] >= ext[2] ? 1 : 2);
+  auto centroid = [&](unsigned int t) {
+    float c = 0.f;
+    for(int k = 0; k < 3; ++k)
+    {
+      const ngl::Vec3 &v = _m.m_vertices[_m.m_triangles[t].m_indices[k]].m_vert;
+      c += axis == 0 ? v.m_x : (axis == 1 ? v.m_y : v.m_z);
+    }
+    return c;
+  };
+  const size_t mid = (_a + _b) / 2;
+  std::nth_element(_ref.begin() + _a, _ref.begin() + mid, _ref.begin() + _b,
+                   [&](unsigned int x, unsigned int y) { return centroid(x) < centroid(y) || (centroid(x) == centroid(y) && x < y); });
+  BVHNode *l = buildTree(_m, _ref, _a, mid);
+  BVHNode *r = buildTree(_m, _ref, mid, _b);
+  return new InnerNode(box, l, r);
+}
+
+// mesh file (tests/test_adapter.py): u32 nv, nt; f32 pos[3nv], nrm[3nv], tan[3nv], uv[2nv]; u32 tris[3nt]
+static bool loadMesh(const char *_path, vMeshData &_m)
+{
+  FILE *f = std::fopen(_path, "rb");
+  if(!f)
+    return false;
+  uint32_t n[2];
+  bool ok = std::fread(n, 4, 2, f) == 2;
+  std::vector<float> pos(3 * n[0]), nrm(3 * n[0]), tan(3 * n[0]), uv(2 * n[0]);
+  std::vector<uint32_t> tris(3 * n[1]);
+  ok = ok && std::fread(pos.data(), 4, pos.size(), f) == pos.size() && std::fread(nrm.data(), 4, nrm.size(), f) == nrm.size() &&
+       std::fread(tan.data(), 4, tan.size(), f) == tan.size() && std::fread(uv.data(), 4, uv.size(), f) == uv.size() &&
+       std::fread(tris.data(), 4, tris.size(), f) == tris.size();
+  std::fclose(f);
+  if(!ok)
+    return false;
+  _m.m_vertices.resize(n[0]);
+  for(uint32_t i = 0; i < n[0]; ++i)
+  {
+    vHVert &v = _m.m_vertices[i];
+    v.m_vert.m_x = pos[3 * i]; v.m_vert.m_y = pos[3 * i + 1]; v.m_vert.m_z = pos[3 * i + 2];
+    v.m_normal.m_x = nrm[3 * i]; v.m_normal.m_y = nrm[3 * i + 1]; v.m_normal.m_z = nrm[3 * i + 2];
+    v.m_tangent.m_x = tan[3 * i]; v.m_tangent.m_y = tan[3 * i + 1]; v.m_tangent.m_z = tan[3 * i + 2];
+    v.m_u = uv[2 * i]; v.m_v = uv[2 * i + 1];
+  }
+  _m.m_triangles.resize(n[1]);
+  for(uint32_t t = 0; t < n[1]; ++t)
+    for(int k = 0; k < 3; ++k)
+      _m.m_triangles[t].m_indices[k] = tris[3 * t + k];
+  _m.m_bvh.m_triIndices.resize(n[1]);
+  for(uint32_t t = 0; t < n[1]; ++t)
+    _m.m_bvh.m_triIndices[t] = t;
+  _m.m_bvh.m_root.reset(buildTree(_m, _m.m_bvh.m_triIndices, 0, n[1]));
+  return true;
+}
+
+static void writeFlat(FILE *_out, const vRendererHIP::FlatMesh &_flat)
+{
+  const uint32_t n[2] = { static_cast<uint32_t>(_flat.bvh.size() / 4), static_cast<uint32_t>(_flat.verts.size() / 4) };
+  std::fwrite(n, 4, 2, _out);
+  for(const std::vector<float> *v : { &_flat.bvh, &_flat.verts, &_flat.normals, &_flat.tangents, &_flat.uvs })
+    std::fwrite(v->data(), 4, v->size(), _out);
+}
+
+// usage: adapter_driver <out>                      Cornell + example sphere, 64x64, 3 frames
+//        adapter_driver <out> <mesh> [--flatten]   Cornell + the mesh (its SBVH flattened by the
+//                                                  adapter); --flatten: only write the flat arrays (no GPU)
 int main(int argc, char **argv)
 {
   if(argc < 2)
     return 2;
+  vMeshData mesh;
+  const bool withMesh = argc >= 3;
+  if(withMesh && !loadMesh(argv[2], mesh))
+    return 3;
+  if(argc >= 4 && std::strcmp(argv[3], "--flatten") == 0)
+  {
+    vRendererHIP::FlatMesh flat;
+    if(!vRendererHIP::flattenSBVH(mesh, flat))
+      return 4;
+    FILE *out = std::fopen(argv[1], "wb");
+    writeFlat(out, flat);
+    std::fclose(out);
+    std::printf("nodes=%zu slots=%zu\n", flat.bvh.size() / 16, flat.verts.size() / 4);
+    return 0;
+  }
   vRendererHIP r;
   r.init(64, 64);
   GLuint tex = 1, depth = 2;
@@ -47,9 +155,11 @@ int main(int argc, char **argv)
   Camera cam;
   r.setCamera(&cam);
   r.useCornellBox(true);
-  r.useExampleSphere(true);
+  r.useExampleSphere(!withMesh);
   r.setFresnelCoef(0.1f);
   r.setFresnelPower(3.f);
+  if(withMesh)
+    r.initMesh(mesh);
   for(int f = 0; f < 3; ++f)
     r.render();
   const unsigned int frames = r.getFrameCount();
@@ -57,6 +167,12 @@ int main(int argc, char **argv)
   FILE *out = std::fopen(argv[1], "wb");
   std::fwrite(&frames, 4, 1, out);
   std::fwrite(g_colour.data(), 1, g_colour.size(), out);
+  if(withMesh)
+  {
+    vRendererHIP::FlatMesh flat;
+    vRendererHIP::flattenSBVH(mesh, flat);
+    writeFlat(out, flat);
+  }
   std::fclose(out);
   std::printf("frames=%u bytes=%zu\n", frames, g_colour.size());
   return 0;

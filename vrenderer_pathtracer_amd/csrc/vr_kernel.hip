@@ -118,7 +118,7 @@ struct HitRec {
 struct Cnt {
     uint32_t rays = 0, nodes = 0, slots = 0, tris = 0, attr = 0, tex = 0, hdr = 0, brdf = 0;
     // instrumented production kernels (F_COUNT_EXEC) only
-    uint32_t nodes_lds = 0, tri_loads = 0, mesh_hits = 0, nmap_hits = 0;
+    uint32_t nodes_lds = 0, tri_loads = 0, mesh_hits = 0, nmap_hits = 0, node_b128 = 0, node_b64 = 0;
 #if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS)
     // diagnostic builds only.  VR_TIMING: per-lane s_memtime cycles in
     // spheres, mesh traversal, hit materialisation, shading, tonemap, whole
@@ -157,7 +157,7 @@ __device__ __forceinline__ void flush_counts(const RenderParams& p, const Cnt& c
 {
     const uint32_t v[kCounters + kExecCounters] = { cnt.rays, cnt.nodes, cnt.slots, cnt.tris, cnt.attr, cnt.tex,
                                                     cnt.hdr, cnt.brdf, cnt.nodes_lds, cnt.tri_loads,
-                                                    cnt.mesh_hits, cnt.nmap_hits };
+                                                    cnt.mesh_hits, cnt.nmap_hits, cnt.node_b128, cnt.node_b64 };
 #pragma unroll
     for (int k = 0; k < kCounters + kExecCounters; ++k) {
         if (k >= kCounters && !exec) break;
@@ -241,11 +241,15 @@ __device__ __forceinline__ int2 buf_load2i(__amdgpu_buffer_rsrc_t b, int off) {
     return make_int2((int)v.x, (int)v.y);
 }
 
-// Conservative fp16 node boxes for the culled traversal (-DVR_FP16_NODES):
-// half the node bytes, but the looser boxes change the visit order, and on
-// C5 one pixel in 8.3 M differed from the strict traversal (fp32 culled: 0),
-// for at most +1.3 % (C3); off by default.
-#ifdef VR_FP16_NODES
+// Conservative fp16 node boxes for the culled traversal (default; -DVR_FP32_NODES
+// keeps the reference's fp32 rows): two 16-B loads per node visit instead of
+// four, the vector-memory instructions this kernel is bound by (C2 +9 %, C3
+// +5 %, C5 +5 % on the 6-wave kernel).  Rounded outward, a box only grows, so
+// no hit is lost; the looser boxes change the visit order, which the exact
+// equal-t tie-break (ref_first) makes irrelevant to the result: images equal
+// the fp32 and the strict traversal bit for bit (C5 differed in one pixel in
+// 8.3 M without it).
+#ifndef VR_FP32_NODES
 constexpr bool kFp16Nodes = true;
 #else
 constexpr bool kFp16Nodes = false;
@@ -341,7 +345,10 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns0) :: "memory");
 #endif
     const bool in_lds = __ballot(node >= L.n_cached) == 0ull;
-    if (COUNT) cnt.nodes_lds += in_lds ? 1u : 0u;
+    if (COUNT) {
+        cnt.nodes_lds += in_lds ? 1u : 0u;
+        if (!in_lds) { cnt.node_b128 += (kFp16Nodes && !strict) ? 2u : 3u; cnt.node_b64 += (kFp16Nodes && !strict) ? 0u : 1u; }
+    }
     if (kFp16Nodes && !strict) {
         // conservative fp16 boxes (lows rounded down, highs up): two 16-B
         // fetches per node instead of four; a box can only grow, so no hit
@@ -500,6 +507,39 @@ __device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, 
     tr.nodeAddr = n == 0 ? top : val[0];
 }
 
+// Equal-t tie-break of the culled traversal.  The reference keeps the first
+// of two triangles hit at exactly the same distance (strict `<`,
+// PathTracer.cu:379), i.e. the one its depth-first walk tests first: slot
+// order inside a leaf; otherwise the child of the two leaves' lowest common
+// ancestor that the walk enters first for this ray -- the nearer by slab entry,
+// child 0 on equal entries (:324-343), computed here with the reference's own
+// (uncontracted) slab arithmetic.  The t-culled walk skips boxes and its
+// contracted slabs can order near-equal children differently, so it asks
+// this whenever a triangle ties the closest hit: any visit order then yields
+// the reference's hit.  Rare (exact fp32 ties: rays through shared edges).
+__device__ __forceinline__ bool ref_first(const RenderParams& p, const Trav& tr, int ka, int kb)
+{
+    const unsigned long long a = p.tpath[ka], b = p.tpath[kb];
+    if (a == b) return ka < kb;                                    // one leaf: slot order
+    const int L = __builtin_ctzll(a ^ b);                          // depth where the paths part
+    const int da = 63 - __builtin_clzll(a), db = 63 - __builtin_clzll(b);
+    if (L >= da || L >= db) return ka < kb;                        // not a tree path (cannot happen)
+    const __amdgpu_buffer_rsrc_t nbuf = buf_rsrc(p.bvh, p.n_nodes * 64u);
+    int off = 0;                                                   // byte offset of the root
+    for (int i = 0; i < L; ++i) {
+        const int2 ni = buf_load2i(nbuf, off + 48);
+        off = (((a >> i) & 1ull) ? ni.y : ni.x) * 16;              // child float4 offset -> bytes
+    }
+    const vr4 n0 = buf_load4(nbuf, off), n1 = buf_load4(nbuf, off + 16), nz = buf_load4(nbuf, off + 32);
+    auto sl = [](float n, float iv, float od) { return n * iv - od; };   // -ffp-contract=off: no FMA
+    const float c0min = span_begin(sl(n0.x, tr.ivx, tr.odx), sl(n0.y, tr.ivx, tr.odx), sl(n0.z, tr.ivy, tr.ody),
+                                   sl(n0.w, tr.ivy, tr.ody), sl(nz.x, tr.ivz, tr.odz), sl(nz.y, tr.ivz, tr.odz), 0.0f);
+    const float c1min = span_begin(sl(n1.x, tr.ivx, tr.odx), sl(n1.y, tr.ivx, tr.odx), sl(n1.z, tr.ivy, tr.ody),
+                                   sl(n1.w, tr.ivy, tr.ody), sl(nz.z, tr.ivz, tr.odz), sl(nz.w, tr.ivz, tr.odz), 0.0f);
+    const unsigned first = (c1min < c0min) ? 1u : 0u;
+    return (unsigned)((a >> L) & 1ull) == first;
+}
+
 // intersectTriangle (RayIntersection.cuh:54-111) for compact triangle k and
 // the closest-hit update (:379-386).  Evaluated branch-free: every early
 // return of the reference becomes a term of the final predicate (the values
@@ -537,6 +577,14 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
         tr.t = dist; tr.best = 3 * k; tr.bu = u; tr.bv = v;
         tr.tcull = strict ? tr.tcull : tr.t * 1.0009765625f;
     }
+#ifndef VR_NO_TIE_ORDER
+    // a tie with the mesh's closest hit so far: keep the reference's first
+    // (the strict walk tests in the reference order already)
+    const bool tie = !strict && ok && dist > VR_EPS && dist == tr.t && tr.best >= 0 && 3 * k != tr.best;
+    if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
+        if (tie && ref_first(p, tr, k, tr.best / 3)) { tr.best = 3 * k; tr.bu = u; tr.bv = v; }
+    }
+#endif
 }
 
 __device__ __forceinline__ TriV tri_load(const RenderParams& p, int k)
@@ -1448,7 +1496,13 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
             VR_LANE(4, 5);
             vr4 out;
             if (bounce_step<CNT, FEAT>(p, ray, hr, ps, out, cnt)) {
+#ifdef VR_PATH_STORE_NT
+                typedef float vr_f32x4 __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(vr_f32x4{ out.x, out.y, out.z, out.w },
+                                            reinterpret_cast<vr_f32x4*>(p.paths + (size_t)q * p.path_stride + slot));
+#else
                 p.paths[(size_t)q * p.path_stride + slot] = out;
+#endif
                 ended = true;
             } else {
                 state = LS_SETUP;

@@ -36,10 +36,11 @@ constexpr int kMaxFramesPerLaunch = 64;
 // lookups.  The instrumented production kernels also fill slots
 // [kExecCounterBase, +kExecCounters): node visits served from the LDS copy,
 // triangle loads issued (36 B each), mesh hits shaded, mesh hits shaded
-// through the normal map.  Slots 8..13 hold diagnostic-build phase timers.
+// through the normal map, 16-B and 8-B lane loads of node visits served from
+// memory.  Slots 8..13 hold diagnostic-build phase timers.
 constexpr int kCounters = 8;
 constexpr int kExecCounterBase = 16;
-constexpr int kExecCounters = 4;
+constexpr int kExecCounters = 6;
 constexpr int kWaveTimesBase = 32;   // -DVR_WAVE_TIMES diagnostic builds: per-wave records from here
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
@@ -83,6 +84,10 @@ struct RenderParams {
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
     const vr3* verts;                // 3 vertices per triangle, compact leaf order (face normal at shading)
     const vr3* tri_e;                // per triangle (v0, v1 - v0, v2 - v0): the traversal's copy
+    // per triangle: its leaf's path from the root of the binary tree (bit i =
+    // child taken at depth i) under a leading 1 bit -- the equal-t tie-break
+    // of the culled traversal (ref_first in vr_kernel.hip)
+    const unsigned long long* tpath;
     uint32_t n_tris;                 // triangles in verts/normals/tangents/uvs
     const vr4* normals;
     const vr4* tangents;

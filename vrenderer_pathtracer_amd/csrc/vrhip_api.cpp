@@ -71,7 +71,7 @@ struct vrhip_ctx {
     bool cornell = false, example = false, view_brdf = false;
     bool strict = false;          // exact reference traversal (no t-culling)
     // mesh
-    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr4* bvh4 = nullptr; vr3* verts = nullptr; vr3* tri_e = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
+    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr4* bvh4 = nullptr; vr3* verts = nullptr; vr3* tri_e = nullptr; unsigned long long* tpath = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
     uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0, dev_nodes4 = 0;
     bool mesh = false;
@@ -162,10 +162,36 @@ struct DeviceMesh {
     std::vector<vr4> nodes4;         // 4-wide nodes, 7 x 16 B each (collapsed binary tree)
     std::vector<vr3> tris;           // packed 12 B vertices (vertex .w never reaches a result)
     std::vector<vr3> tri_e;          // per triangle v0, v1 - v0, v2 - v0 (fp32, the kernel's own subtractions)
+    std::vector<unsigned long long> tpath;   // per triangle: leaf path from the root under a leading 1 bit
     std::vector<vr2> uvs;
 };
 
 constexpr int kLeafCountBits = 7;
+
+// Per compact triangle, the path from the root to its leaf (bit i = the child
+// taken at depth i) under a leading 1 bit: the key the kernel's equal-t
+// tie-break (ref_first) uses to find the two leaves' lowest common ancestor.
+// Paths depend only on the tree's shape, so the node renumbering below keeps them.
+void tri_paths(DeviceMesh& dm)
+{
+    dm.tpath.assign(std::max<size_t>(dm.tris.size() / 3, 1), 0ull);
+    if (dm.nodes.empty()) return;
+    struct Item { size_t off; unsigned long long bits; int depth; };
+    std::vector<Item> st{ { 0, 0ull, 0 } };
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        for (int ch = 0; ch < 2; ++ch) {
+            int32_t idx;
+            std::memcpy(&idx, &dm.nodes[it.off + 3].x + ch, 4);
+            const unsigned long long bits = it.bits | ((unsigned long long)ch << it.depth);
+            if (idx >= 0) { st.push_back({ (size_t)idx, bits, it.depth + 1 }); continue; }
+            const uint32_t code = (uint32_t)~idx;
+            const uint32_t first = code >> kLeafCountBits, count = code & ((1u << kLeafCountBits) - 1u);
+            for (uint32_t t = first; t < first + count; ++t) dm.tpath[t] = (1ull << (it.depth + 1)) | bits;
+        }
+    }
+}
 
 // Renumbers the inner nodes so that node i is the i-th largest box by surface
 // area (a parent always precedes its children; the root stays at 0).  The
@@ -418,6 +444,7 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
             std::memcpy(&idxf[ch], &code, 4);
         }
     }
+    tri_paths(dm);
 #ifndef VR_NO_AREA_ORDER
     order_nodes_by_area(dm);
 #endif
@@ -531,7 +558,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     quiesce(c);
     dfree(c->accum); dfree(c->rgba); dfree(c->depth);
-    dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->verts); dfree(c->tri_e); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
+    dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->verts); dfree(c->tri_e); dfree(c->tpath); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     for (int i = 0; i < 2; ++i)
         if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
@@ -617,6 +644,7 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     c->dev_nodes4 = (uint32_t)(dm.nodes4.size() / 7);
     if ((rc = upload(c, c->verts, dm.tris.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->tri_e, dm.tri_e.data(), nt * sizeof(vr3)))) return rc;
+    if ((rc = upload(c, c->tpath, dm.tpath.data(), dm.tpath.size() * sizeof(unsigned long long)))) return rc;
     if ((rc = upload(c, c->normals, dm.normals.data(), nt * 16))) return rc;
     if ((rc = upload(c, c->tangents, dm.tangents.data(), nt * 16))) return rc;
     if ((rc = upload(c, c->uvs, dm.uvs.data(), nt * 8))) return rc;
@@ -890,7 +918,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.tiles_x = p.wr / 16u;
     p.rank = c->rank; p.nranks = c->nranks;
     p.bvh4 = c->bvh4; p.n_nodes4 = c->mesh ? c->dev_nodes4 : 0;
-    p.bvh = c->bvh; p.bvh16 = c->bvh16; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.tri_e = c->tri_e; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
+    p.bvh = c->bvh; p.bvh16 = c->bvh16; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.tri_e = c->tri_e; p.tpath = c->tpath; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
     p.hdr = c->hdr; p.hdr_w = c->hdr_w; p.hdr_h = c->hdr_h;
     for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
     p.brdf = c->brdf;
