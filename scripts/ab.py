@@ -50,11 +50,17 @@ def main():
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--strict", action="store_true")
+    ap.add_argument("--leaf", type=int, default=None, help="max triangles per leaf of the scene's BVH")
+    ap.add_argument("--node-cost", type=float, default=None, help="SAH node cost of the scene's BVH")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     results = {}
     for lib in a.libs:
         env = dict(os.environ, VRHIP_LIB=os.path.abspath(lib))
+        if a.leaf:
+            env["VRHIP_MAX_LEAF"] = str(a.leaf)
+        if a.node_cost is not None:
+            env["VRHIP_SAH_NODE_COST"] = str(a.node_cost)
         code = CHILD.format(repo=REPO, cfg=a.cfg, frames=a.frames, steps=a.steps, strict=a.strict)
         p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
         if p.returncode != 0:

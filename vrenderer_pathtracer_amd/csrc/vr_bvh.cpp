@@ -56,6 +56,7 @@ struct Builder {
     const float* pos;
     const uint32_t* tris;
     uint32_t max_leaf;
+    double node_cost = 1.0;              // SAH traversal cost per node (triangle test = 1)
     uint32_t max_depth;
     std::vector<Box> tri_box;
     std::vector<float> centroid;       // 3 per triangle
@@ -174,7 +175,7 @@ struct Builder {
         }
         const double parent_area = b.area();
         // SAH: C_node + (A_L N_L + A_R N_R) / A_P * C_tri  vs  N * C_tri
-        const double split_cost = VR_BVH_NODE_COST + (parent_area > 0.0 ? best_cost / parent_area : (double)count);
+        const double split_cost = node_cost + (parent_area > 0.0 ? best_cost / parent_area : (double)count);
         const bool want_leaf = count <= max_leaf && (best_axis < 0 || split_cost >= (double)count);
         if (!force_split && want_leaf) return make_leaf(first, count, b);
 
@@ -248,6 +249,11 @@ int build_flat(const float* positions, const float* normals, const float* tangen
 #else
     B.max_leaf = max_leaf_tris ? max_leaf_tris : 4;
 #endif
+    B.node_cost = VR_BVH_NODE_COST;
+    // VRHIP_SAH_NODE_COST: builder experiments (node visit vs triangle test
+    // cost); the tree changes only speed -- and the order of exactly tied
+    // triangles, which the oracle reproduces from the same flattened tree
+    if (const char* e = std::getenv("VRHIP_SAH_NODE_COST")) B.node_cost = std::atof(e);
     B.max_depth = kMaxBuildDepth;
     B.tri_box.resize(n_tris);
     B.centroid.resize(3 * (size_t)n_tris);

@@ -20,6 +20,7 @@ on the GPU box.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 
@@ -167,7 +168,9 @@ def synthetic_merl() -> np.ndarray:
 _MESH_CACHE: dict = {}
 
 
-def knot_flat(nu: int, nv: int, max_leaf_tris: int = 4) -> dict:
+def knot_flat(nu: int, nv: int, max_leaf_tris: int = None) -> dict:
+    if max_leaf_tris is None:       # VRHIP_MAX_LEAF: builder experiments (scripts/ab.py --leaf)
+        max_leaf_tris = int(os.environ.get("VRHIP_MAX_LEAF", "4"))
     key = (nu, nv, max_leaf_tris)
     if key not in _MESH_CACHE:
         _MESH_CACHE[key] = build_flat(torus_knot(nu, nv), max_leaf_tris=max_leaf_tris)
