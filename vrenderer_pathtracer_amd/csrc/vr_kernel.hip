@@ -207,9 +207,16 @@ constexpr int kLeafCountBits = 7;
 #define VR_LDS_BUDGET (40960 - 256)
 #endif
 constexpr int kLdsBudget = VR_LDS_BUDGET;
+#ifndef VR_STACK_CULL_MAX
+#define VR_STACK_CULL_MAX 0    // stack classes <= this carry entry distances (6 B per entry instead of 4);
+                               // off: measured C2 -13 %, C3 -8 % (16-entry class), and the
+                               // 24-entry stacks of C5 would not fit two 768-thread blocks per CU
+#endif
+constexpr bool stack_cull(int stack) { return stack <= VR_STACK_CULL_MAX; }
+constexpr int stack_entry_bytes(int stack) { return stack_cull(stack) ? 6 : 4; }
 constexpr int cache_nodes(int stack, int extra = 0, int bt = kBlockThreads) {
-    return ((bt / kBlockThreads) * kLdsBudget - stack * bt * 4 - extra) / 56 > 0 ?
-           ((bt / kBlockThreads) * kLdsBudget - stack * bt * 4 - extra) / 56 : 1;
+    return ((bt / kBlockThreads) * kLdsBudget - stack * bt * stack_entry_bytes(stack) - extra) / 56 > 0 ?
+           ((bt / kBlockThreads) * kLdsBudget - stack * bt * stack_entry_bytes(stack) - extra) / 56 : 1;
 }
 // Raw buffer loads for the node and triangle arrays: a 32-bit lane offset
 // against an SGPR descriptor (bounds-checked, no 64-bit address math), and an
@@ -257,6 +264,7 @@ constexpr bool kFp16Nodes = false;
 
 struct Lds {
     int* stk;                 // this thread's column of the stack
+    unsigned short* tstk;     // entry distance of each stacked child (bf16, rounded down)
     const vr4* nodes;         // fp32 nodes: 3 rows per cached node; fp16 nodes: 2 rows per node
     const int2* idx;          // fp32 nodes: child indices per cached node
     int n_cached;             // nodes [0, n_cached) are read from LDS
@@ -272,17 +280,26 @@ struct Trav {
     float ivx, ivy, ivz, odx, ody, odz;
     float t, tcull, bu, bv;
     int best, sp, nodeAddr;
-    int top;                  // register copy of the stack top, stk[sp]
+    float tcur;               // slab entry of nodeAddr's box (a lower bound; 0 for the root)
     int k, kend;              // leaf in progress (trav_step only)
 };
 
-template <uint32_t FEAT>
+// Stacked children carry their slab entry distance, rounded down to bf16
+// (the high half of a non-negative float's bits): a popped subtree or leaf
+// whose entry already lies beyond the closest hit (tcull) is skipped without
+// fetching it -- the same test that culls a child when it is first met, made
+// again with the closest hit found since.  Strict mode never culls.
+__device__ __forceinline__ unsigned short tkey(float t) { return (unsigned short)(__float_as_uint(t) >> 16); }
+__device__ __forceinline__ float tkey_f(unsigned short k) { return __uint_as_float((uint32_t)k << 16); }
+
+template <uint32_t FEAT, bool SC>
 __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, float t0, Trav& tr, const Lds& L)
 {
     tr.sp = 0;
     L.stk[0] = kSentinel;
-    tr.top = kSentinel;
+    if (SC) L.tstk[0] = 0;
     tr.nodeAddr = 0;
+    tr.tcur = 0.f;
     // invDir (PathTracer.cu:289-294): components with |d| <= eps become +eps,
     // so |d| >= eps > 2^-32 and rcp_rn is the IEEE quotient unless a
     // component exceeds 2^125 (then the wave divides)
@@ -310,33 +327,32 @@ __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, f
 // One outer iteration: the inner node loop until this lane holds a leaf and
 // the wave agrees (ballot), then the leaf loop.  Precondition: tr.nodeAddr is
 // an inner node (not kSentinel).
-// Pop (:339-342 and the leaf-loop pops): the top is already in a register;
-// the entry below it is read for the next pop, off the critical path.  sp
-// reaches -1 only by popping the sentinel, after which nothing is popped.
+// Pop (:339-342 and the leaf-loop pops), with the popped entry's distance in
+// tr.tcur.  sp reaches -1 only by popping the sentinel, after which nothing
+// is popped.
+template <bool SC>
 __device__ __forceinline__ int trav_pop(Trav& tr, const Lds& L)
 {
-#ifdef VR_TOP_IN_REG
-    const int v = tr.top;
-    --tr.sp;
-    tr.top = L.stk[(tr.sp > 0 ? tr.sp : 0) * L.stride];
-    return v;
-#else
-    return L.stk[(tr.sp--) * L.stride];
-#endif
+    const int i = (tr.sp--) * L.stride;
+    tr.tcur = SC ? tkey_f(L.tstk[i]) : 0.f;
+    return L.stk[i];
 }
 
 // One inner-node visit (:295-343): fetch (LDS copy or L2/HBM), two slab
 // tests, near child next, far child pushed when both are entered, pop when
 // neither is.  Leaves in tr.nodeAddr are left to the caller.
-template <bool COUNT, uint32_t FEAT>
+template <bool COUNT, uint32_t FEAT, bool SC>
 __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
     int* stk = L.stk;
     const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
-    if (COUNT) cnt.nodes++;
+    // a popped node whose box starts beyond the closest hit: not fetched,
+    // treated as entering neither child (pop the next)
+    const bool dead = SC && tr.tcur > tr.tcull;
+    if (COUNT) cnt.nodes += dead ? 0u : 1u;
     VR_LANE(0, 1);
-    vr4 n0, n1, nz;
-    int idx0, idx1;
+    vr4 n0 = mk4(0.f, 0.f, 0.f, 0.f), n1 = n0, nz = n0;
+    int idx0 = 0, idx1 = 0;
     const int node = tr.nodeAddr >> 2;
     // wave-uniform choice between the LDS copy and L2/HBM: a diverged wave
     // would pay both round trips
@@ -344,12 +360,13 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     uint64_t ns0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns0) :: "memory");
 #endif
-    const bool in_lds = __ballot(node >= L.n_cached) == 0ull;
-    if (COUNT) {
+    const bool in_lds = __ballot(!dead && node >= L.n_cached) == 0ull;
+    if (COUNT && !dead) {
         cnt.nodes_lds += in_lds ? 1u : 0u;
         if (!in_lds) { cnt.node_b128 += (kFp16Nodes && !strict) ? 2u : 3u; cnt.node_b64 += (kFp16Nodes && !strict) ? 0u : 1u; }
     }
-    if (kFp16Nodes && !strict) {
+    if (dead) {
+    } else if (kFp16Nodes && !strict) {
         // conservative fp16 boxes (lows rounded down, highs up): two 16-B
         // fetches per node instead of four; a box can only grow, so no hit
         // the exact box admits is lost
@@ -420,14 +437,16 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     // keep the child-index load in the same round trip as the bounds
     asm volatile("" ::"v"(idx0), "v"(idx1));
     const bool swp = (c1min < c0min);
-    const bool tc0 = (c0max >= c0min) && (c0min <= tr.tcull);
-    const bool tc1 = (c1max >= c1min) && (c1min <= tr.tcull);
+    const bool tc0 = !dead && (c0max >= c0min) && (c0min <= tr.tcull);
+    const bool tc1 = !dead && (c1max >= c1min) && (c1min <= tr.tcull);
     // branch-free push/pop: near child next, far child pushed when both
     // are hit, pop when neither is (same order as :324-343)
     const bool both = tc0 && tc1;
     const bool none = !tc0 && !tc1;
     const int nearc = (both && swp) ? idx1 : (tc0 ? idx0 : idx1);
     const int farc = swp ? idx0 : idx1;
+    const float near_t = (both && swp) ? c1min : (tc0 ? c0min : c1min);
+    const float far_t = swp ? c0min : c1min;
 #ifdef VR_NODE_STAMPS
     {
         uint64_t ns2;
@@ -435,21 +454,15 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
         cnt.tm[1] += ns2 - ns1;
     }
 #endif
-#ifdef VR_TOP_IN_REG
-    // branch-free, stack top in a register: the entry below the new top is
-    // read every visit but only consumed by a later pop
-    const int popped = tr.top;
-    if (both) stk[(tr.sp + 1) * L.stride] = farc;
-    tr.sp += both ? 1 : (none ? -1 : 0);
-    tr.nodeAddr = none ? popped : nearc;
-    const int below = stk[(tr.sp > 0 ? tr.sp : 0) * L.stride];
-    tr.top = both ? farc : (none ? below : tr.top);
-#else
     const int top = stk[tr.sp * L.stride];
-    if (both) stk[(tr.sp + 1) * L.stride] = farc;
+    const float ttop = SC ? tkey_f(L.tstk[tr.sp * L.stride]) : 0.f;
+    if (both) {
+        stk[(tr.sp + 1) * L.stride] = farc;
+        if (SC) L.tstk[(tr.sp + 1) * L.stride] = tkey(far_t);
+    }
     tr.sp += both ? 1 : (none ? -1 : 0);
     tr.nodeAddr = none ? top : nearc;
-#endif
+    tr.tcur = SC ? (none ? ttop : near_t) : 0.f;
 }
 
 // One visit of a 4-wide node (F_WIDE, t-culled mode only): four slab tests
@@ -458,7 +471,7 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
 // far to near.  Visits half as many nodes per ray as the binary walk; the
 // closest hit is the same (only the order among equal-distance hits can
 // differ, as for any culled order).
-template <bool COUNT, uint32_t FEAT>
+template <bool COUNT, uint32_t FEAT, bool SC>
 __device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
     int* stk = L.stk;
@@ -498,13 +511,15 @@ __device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, 
     };
     cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
     const int top = stk[tr.sp * L.stride];
-    if (n >= 4) stk[(tr.sp + 1) * L.stride] = val[3];
+    const float ttop = SC ? tkey_f(L.tstk[tr.sp * L.stride]) : 0.f;
+    if (n >= 4) { stk[(tr.sp + 1) * L.stride] = val[3]; if (SC) L.tstk[(tr.sp + 1) * L.stride] = tkey(key[3]); }
     tr.sp += n >= 4 ? 1 : 0;
-    if (n >= 3) stk[(tr.sp + 1) * L.stride] = val[2];
+    if (n >= 3) { stk[(tr.sp + 1) * L.stride] = val[2]; if (SC) L.tstk[(tr.sp + 1) * L.stride] = tkey(key[2]); }
     tr.sp += n >= 3 ? 1 : 0;
-    if (n >= 2) stk[(tr.sp + 1) * L.stride] = val[1];
+    if (n >= 2) { stk[(tr.sp + 1) * L.stride] = val[1]; if (SC) L.tstk[(tr.sp + 1) * L.stride] = tkey(key[1]); }
     tr.sp += n >= 2 ? 1 : (n == 0 ? -1 : 0);
     tr.nodeAddr = n == 0 ? top : val[0];
+    tr.tcur = SC ? (n == 0 ? ttop : key[0]) : 0.f;
 }
 
 // Equal-t tie-break of the culled traversal.  The reference keeps the first
@@ -620,13 +635,16 @@ __device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Tr
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
+    constexpr bool SC = stack_cull(STACK);
     int leafAddr = 0;
+    float leafT = 0.f;                                          // slab entry of the postponed leaf
     while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
-        if (HAS(F_WIDE)) node_step4<COUNT, FEAT>(p, r, tr, L, cnt);
-        else node_step<COUNT, FEAT>(p, r, tr, L, cnt);
+        if (HAS(F_WIDE)) node_step4<COUNT, FEAT, SC>(p, r, tr, L, cnt);
+        else node_step<COUNT, FEAT, SC>(p, r, tr, L, cnt);
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
             leafAddr = tr.nodeAddr;
-            tr.nodeAddr = trav_pop(tr, L);
+            leafT = tr.tcur;
+            tr.nodeAddr = trav_pop<SC>(tr, L);
         }
         // the wave moves on to the leaves once (nearly) every lane holds one;
         // lanes still searching resume in the next outer iteration
@@ -634,7 +652,9 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
     }
     while (leafAddr < 0) {
         const int lv = ~leafAddr;
-        const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
+        // a leaf whose box starts beyond the closest hit found since it was
+        // met holds no closer triangle: skipped
+        const int kend = (lv >> kLeafCountBits) + ((SC && leafT > tr.tcull) ? 0 : (lv & ((1 << kLeafCountBits) - 1)));
 #ifndef VR_NO_TRI_PAIRS
         // the loads of two triangles in one trip (the tests stay in slot order):
         // a leaf's triangles need half the dependent round trips (C2 +1 %, C3 +4 %)
@@ -650,7 +670,8 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         for (int k = lv >> kLeafCountBits; k < kend; ++k) tri_test<COUNT, FEAT>(p, r, tr, k, cnt);
 #endif
         leafAddr = tr.nodeAddr;
-        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop(tr, L);
+        leafT = tr.tcur;
+        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop<SC>(tr, L);
     }
 }
 
@@ -665,13 +686,13 @@ __device__ __forceinline__ void trav_step(const RenderParams& p, const Ray& r, T
         tri_test<COUNT, FEAT>(p, r, tr, tr.k, cnt);
         ++tr.k;
     } else {
-        node_step<COUNT, FEAT>(p, r, tr, L, cnt);
+        node_step<COUNT, FEAT, false>(p, r, tr, L, cnt);
     }
     if (tr.k >= tr.kend && tr.nodeAddr < 0) {                // start the leaf, resume at the stack top
         const int lv = ~tr.nodeAddr;
         tr.k = lv >> kLeafCountBits;
         tr.kend = tr.k + (lv & ((1 << kLeafCountBits) - 1));
-        tr.nodeAddr = trav_pop(tr, L);
+        tr.nodeAddr = trav_pop<false>(tr, L);
     }
 }
 
@@ -684,7 +705,7 @@ template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
 {
     Trav tr;
-    trav_init<FEAT>(p, r, hr.t, tr, L);
+    trav_init<FEAT, stack_cull(STACK)>(p, r, hr.t, tr, L);
     while (tr.nodeAddr != kSentinel) trav_iter<STACK, COUNT, FEAT>(p, r, tr, L, cnt);
     trav_finish(tr, hr);
 }
@@ -1113,11 +1134,13 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
 // Binds this thread's stack column and fills the block's node cache with
 // the first nodes of the area-ordered node array.
 template <uint32_t FEAT, int BT = kBlockThreads>
-__device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, vr4* lds_nodes, int2* lds_idx,
+__device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, unsigned short* lds_tstk,
+                                         vr4* lds_nodes, int2* lds_idx,
                                          int cn, int tid)
 {
     Lds L;
     L.stk = lds_stack + tid;
+    L.tstk = lds_tstk + tid;
     L.stride = BT;
     L.nodes = lds_nodes;
     L.idx = lds_idx;
@@ -1162,10 +1185,11 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
 {
     constexpr int CN = cache_nodes(STACK);
     __shared__ int lds_stack[STACK * kBlockThreads];
+    __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * kBlockThreads : 1];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
     const int tid = threadIdx.x;
-    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
+    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, tid);
     // block -> (tile, path group): the 2*n_frames paths of a pixel are split
     // into p.split contiguous groups run by different blocks (strong-scaling
     // and tail balance); group g of tile t is block t*split + g
@@ -1254,9 +1278,11 @@ template <int STACK, uint32_t FEAT>
 __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderParams p)
 {
     __shared__ int lds_stack[STACK * kBlockThreads];
+    __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * kBlockThreads : 1];
     const int tid = threadIdx.x;
     Lds L;
     L.stk = lds_stack + tid;
+    L.tstk = lds_tstk + tid;
     L.stride = kBlockThreads;
     L.nodes = nullptr;
     L.idx = nullptr;
@@ -1340,8 +1366,8 @@ constexpr int path_blocks_per_cu(int stack, int bt) { return 4 * path_waves(stac
 // LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
 // the node cache takes what the stacks leave (56 B per node)
 constexpr int path_cache_nodes(int stack, int bt) {
-    return (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * 4) / 56 > 0
-               ? (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * 4) / 56 : 1;
+    return (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)) / 56 > 0
+               ? (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)) / 56 : 1;
 }
 
 #ifndef VR_XCD_BANDS
@@ -1353,10 +1379,11 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
 {
     constexpr int CN = path_cache_nodes(STACK, BT);
     __shared__ int lds_stack[STACK * BT];
+    __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * BT : 1];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
     const int tid = threadIdx.x;
-    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
+    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, tid);
     const int lane = tid & 63;
     const uint32_t n_paths = 2u * p.n_frames;
     const uint32_t n_sub = p.path_stride >> 6;             // 8x8 sub-tiles of the rank's tiles
@@ -1456,7 +1483,7 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
         VR_T0(t_setup);
         if (state == LS_SETUP) {
             if (intersect_spheres<CNT, FEAT>(p, ray, hr, cnt)) {
-                trav_init<FEAT>(p, ray, hr.t, tr, L);
+                trav_init<FEAT, stack_cull(STACK)>(p, ray, hr.t, tr, L);
                 state = LS_TRAV;
             } else {
                 state = LS_SHADE;
