@@ -260,7 +260,7 @@ void vRendererHIP::initMesh(const vMeshData &_meshData)
     for(int k = 0; k < 3; ++k)
       tris[3 * i + k] = _meshData.m_triangles[i].m_indices[k];
   validate(vrhip_upload_mesh_indexed(m_ctx, pos.data(), nrm.data(), tan.data(), uv.data(),
-                                     static_cast<uint32_t>(nv), tris.data(), static_cast<uint32_t>(nt), 4),
+                                     static_cast<uint32_t>(nv), tris.data(), static_cast<uint32_t>(nt), 2),
            "Upload mesh");
 }
 

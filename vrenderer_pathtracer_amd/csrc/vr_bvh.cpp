@@ -247,7 +247,7 @@ int build_flat(const float* positions, const float* normals, const float* tangen
     (void)max_leaf_tris;
     B.max_leaf = VR_BVH_MAX_LEAF;
 #else
-    B.max_leaf = max_leaf_tris ? max_leaf_tris : 4;
+    B.max_leaf = max_leaf_tris ? max_leaf_tris : 2;
 #endif
     B.node_cost = VR_BVH_NODE_COST;
     // VRHIP_SAH_NODE_COST: builder experiments (node visit vs triangle test

@@ -37,7 +37,7 @@ def _f32(a, shape=None):
     return a
 
 
-def build_flat(mesh: dict, max_leaf_tris: int = 4) -> dict:
+def build_flat(mesh: dict, max_leaf_tris: int = 2) -> dict:
     """Native BVH build + reference flattening (src/vRendererCuda.cpp:204-279).
 
     mesh: positions (N,3), normals (N,3), tangents (N,3), uvs (N,2), tris (M,3) uint32.

@@ -169,8 +169,12 @@ _MESH_CACHE: dict = {}
 
 
 def knot_flat(nu: int, nv: int, max_leaf_tris: int = None) -> dict:
-    if max_leaf_tris is None:       # VRHIP_MAX_LEAF: builder experiments (scripts/ab.py --leaf)
-        max_leaf_tris = int(os.environ.get("VRHIP_MAX_LEAF", "4"))
+    # leaves of <= 2 triangles (one paired load per leaf) for the 10k knot:
+    # C2 +4 % over 4 with the fp16-node kernel, C3 within noise; the 1M knot
+    # (C5, triangles streamed from HBM) keeps 4 (2: -2 %) (scripts/gpu_bvh_sweep.sh).
+    # VRHIP_MAX_LEAF overrides it for builder experiments (scripts/ab.py --leaf)
+    if max_leaf_tris is None:
+        max_leaf_tris = int(os.environ.get("VRHIP_MAX_LEAF", "2" if nu * nv * 2 <= 100000 else "4"))
     key = (nu, nv, max_leaf_tris)
     if key not in _MESH_CACHE:
         _MESH_CACHE[key] = build_flat(torus_knot(nu, nv), max_leaf_tris=max_leaf_tris)
