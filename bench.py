@@ -95,20 +95,14 @@ def reference_bytes(c: dict, paths: int, pixel_frames: int) -> float:
             + 16 * c["tex_fetches"] + 16 * c["hdr_fetches"] + 12 * c["brdf_fetches"] + 92 * pixel_frames)
 
 
-def executed_loads(e: dict, paths: int, wave_kernel: bool) -> dict:
-    """Per-lane global loads the production render kernels issue, by width
-    (bytes): the node visits not served from LDS (counted by width in the
-    kernel: 2x16 per conservative fp16 node, 3x16 + 8 per fp32 node);
-    triangles 3x12 (v0, two edges) per triangle load; per mesh hit shaded uv
-    3x8 + tangents 3x16 + normals 3x16 (normal map) or vertices 3x12 (face
-    normal); 16 per texture / HDRI texel; 3x4 per BRDF lookup; 2x16 primary
-    record per path (path kernel)."""
-    hits, nmap = e["mesh_hits"], e["nmap_hits"]
-    return {16: e["node_lane_loads_b128"] + 3 * hits + 3 * nmap + e["tex_fetches"] + e["hdr_fetches"]
-            + (2 * paths if wave_kernel else 0),
-            12: 3 * e["tri_loads"] + 3 * (hits - nmap),
-            8: e["node_lane_loads_b64"] + 3 * hits,
-            4: 3 * e["brdf_fetches"]}
+def executed_loads(e: dict) -> dict:
+    """Per-lane global loads the production render kernels issue, by width in
+    bytes, as counted at every load site by the instrumented kernels: node
+    visits not served from LDS (2x16 B per conservative fp16 node), triangle
+    pairs (4x16 + 8 B), primary records (2x16 B per path), hit attributes
+    (uv 3x8, tangents / normals 3x16, face-normal vertices 3x12 -- those the
+    scene's specialised kernel loads), texels and HDRI (16 B), BRDF entries (4 B)."""
+    return {16: e["lane_loads_b128"], 12: e["lane_loads_b96"], 8: e["lane_loads_b64"], 4: e["lane_loads_b32"]}
 
 
 def vmem_roof(device: int) -> dict:
@@ -348,9 +342,9 @@ def main():
     if rank == 0:
         own_paths = owned * 2 * F
         avg_launch_s = (kms / 1e3) / max(launches, 1)
-        loads = executed_loads(exec_counts, own_paths, mesh)
+        loads = executed_loads(exec_counts)
         load_bytes = sum(w * n for w, n in loads.items())
-        lds_bytes = (32 if exec_counts["node_lane_loads_b64"] == 0 else 56) * exec_counts["node_visits_lds"]
+        lds_bytes = 32 * exec_counts["node_visits_lds"]        # fp16 node rows from the LDS copy
         store_bytes = 16 * own_paths + (32 * owned if mesh else 0)
         ref_b = reference_bytes(ref_counts, own_paths, owned * F)
         achieved = load_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0

@@ -171,10 +171,11 @@ int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *time
  * reads), then [8] node visits served from the block's LDS copy of the tree
  * top, [9] triangle loads issued
  * (36 B each; an odd leaf's last pair loads its triangle twice), [10] mesh
- * hits shaded, [11] of those through the normal map, [12] / [13] 16-B / 8-B
- * lane loads of the node visits served from memory (fp32 nodes: 3 + 1 per
- * visit; the default conservative fp16 nodes: 2 + 0).  Synchronous. */
-#define VRHIP_PROFILE_COUNTERS 14
+ * hits shaded, [11] of those through the normal map, [12..15] every global
+ * lane load the production kernels issue, by width: 16 B, 12 B, 8 B, 4 B
+ * (nodes, triangles, primary records, attributes, texels, BRDF entries).
+ * Synchronous. */
+#define VRHIP_PROFILE_COUNTERS 16
 int vrhip_render_profiled(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
                           uint64_t counters[VRHIP_PROFILE_COUNTERS]);
 int vrhip_sync(vrhip_ctx *ctx);

@@ -118,7 +118,8 @@ struct HitRec {
 struct Cnt {
     uint32_t rays = 0, nodes = 0, slots = 0, tris = 0, attr = 0, tex = 0, hdr = 0, brdf = 0;
     // instrumented production kernels (F_COUNT_EXEC) only
-    uint32_t nodes_lds = 0, tri_loads = 0, mesh_hits = 0, nmap_hits = 0, node_b128 = 0, node_b64 = 0;
+    // and its lane loads by width (16 / 12 / 8 / 4 B) at every global-load site
+    uint32_t nodes_lds = 0, tri_loads = 0, mesh_hits = 0, nmap_hits = 0, ld128 = 0, ld96 = 0, ld64 = 0, ld32 = 0;
 #if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS)
     // diagnostic builds only.  VR_TIMING: per-lane s_memtime cycles in
     // spheres, mesh traversal, hit materialisation, shading, tonemap, whole
@@ -157,7 +158,8 @@ __device__ __forceinline__ void flush_counts(const RenderParams& p, const Cnt& c
 {
     const uint32_t v[kCounters + kExecCounters] = { cnt.rays, cnt.nodes, cnt.slots, cnt.tris, cnt.attr, cnt.tex,
                                                     cnt.hdr, cnt.brdf, cnt.nodes_lds, cnt.tri_loads,
-                                                    cnt.mesh_hits, cnt.nmap_hits, cnt.node_b128, cnt.node_b64 };
+                                                    cnt.mesh_hits, cnt.nmap_hits, cnt.ld128, cnt.ld96, cnt.ld64,
+                                                    cnt.ld32 };
 #pragma unroll
     for (int k = 0; k < kCounters + kExecCounters; ++k) {
         if (k >= kCounters && !exec) break;
@@ -360,10 +362,14 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     uint64_t ns0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns0) :: "memory");
 #endif
+#ifdef VR_LDS_PER_LANE
+    const bool in_lds = node < L.n_cached;                       // per lane: both paths may issue
+#else
     const bool in_lds = __ballot(!dead && node >= L.n_cached) == 0ull;
+#endif
     if (COUNT && !dead) {
         cnt.nodes_lds += in_lds ? 1u : 0u;
-        if (!in_lds) { cnt.node_b128 += (kFp16Nodes && !strict) ? 2u : 3u; cnt.node_b64 += (kFp16Nodes && !strict) ? 0u : 1u; }
+        if (!in_lds) { cnt.ld128 += (kFp16Nodes && !strict) ? 2u : 3u; cnt.ld64 += (kFp16Nodes && !strict) ? 0u : 1u; }
     }
     if (dead) {
     } else if (kFp16Nodes && !strict) {
@@ -619,7 +625,7 @@ template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Trav& tr, int k, Cnt& cnt)
 {
     const TriV t = tri_load(p, k);
-    if (COUNT) cnt.tri_loads++;
+    if (COUNT) { cnt.tri_loads++; cnt.ld96 += 3; }
     asm volatile("" ::"v"(t.a0.x), "v"(t.a1.x), "v"(t.a2.x));   // three dwordx3 loads, one trip
     tri_test_v<COUNT, FEAT>(p, r, tr, k, t, cnt);
 }
@@ -628,6 +634,11 @@ __device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Tr
 // this lane holds a leaf and the wave agrees (ballot, :353-363), with one
 // leaf postponed (:345-351), then the leaf loop.  Precondition: tr.nodeAddr
 // is an inner node (not kSentinel).
+// Paired triangle loads as 4 x 16 B + 8 B over the pair's 72 contiguous bytes
+// (5 vector loads instead of 6: C2 +1 %, C3 +1 %, C5 +3 %); -DVR_TRI_B96 keeps 3 x 12 B per triangle.
+#ifndef VR_TRI_B96
+#define VR_TRI_B128
+#endif
 #ifndef VR_NODE_BREAK
 #define VR_NODE_BREAK 6    // measured (path kernel with paired triangle loads): 0 (the reference's
                            // all-lanes vote) C2 2,294, 2: 2,503, 4: 2,563, 6: 2,577, 8: 2,583 (C3 -2 %)
@@ -660,8 +671,31 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         // a leaf's triangles need half the dependent round trips (C2 +1 %, C3 +4 %)
         for (int k = lv >> kLeafCountBits; k < kend; k += 2) {
             const bool two = k + 1 < kend;
+#ifdef VR_TRI_B128
+            // the pair's 72 contiguous bytes as 4 x 16 B + 8 B (5 loads instead of 6);
+            // past the array end the buffer descriptor returns zeros (never tested)
+            TriV ta, tb;
+            {
+                const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, p.n_tris * 36u);
+                const int o = k * 36;
+                const vr4 q0 = buf_load4(tbuf, o), q1 = buf_load4(tbuf, o + 16), q2 = buf_load4(tbuf, o + 32),
+                          q3 = buf_load4(tbuf, o + 48);
+                const int2 q4 = buf_load2i(tbuf, o + 64);
+                ta.a0 = vr3{ q0.x, q0.y, q0.z }; ta.a1 = vr3{ q0.w, q1.x, q1.y }; ta.a2 = vr3{ q1.z, q1.w, q2.x };
+                tb.a0 = vr3{ q2.y, q2.z, q2.w }; tb.a1 = vr3{ q3.x, q3.y, q3.z };
+                tb.a2 = vr3{ q3.w, __int_as_float(q4.x), __int_as_float(q4.y) };
+            }
+#else
             const TriV ta = tri_load(p, k), tb = tri_load(p, two ? k + 1 : k);
-            if (COUNT) cnt.tri_loads += 2;                      // an odd leaf's last pair loads its triangle twice
+#endif
+            if (COUNT) {                                        // an odd leaf's last pair loads its triangle twice
+                cnt.tri_loads += 2;
+#ifdef VR_TRI_B128
+                cnt.ld128 += 4; cnt.ld64 += 1;
+#else
+                cnt.ld96 += 6;
+#endif
+            }
             asm volatile("" ::"v"(ta.a0.x), "v"(ta.a1.x), "v"(ta.a2.x), "v"(tb.a0.x), "v"(tb.a1.x), "v"(tb.a2.x));
             tri_test_v<COUNT, FEAT>(p, r, tr, k, ta, cnt);
             if (two) tri_test_v<COUNT, FEAT>(p, r, tr, k + 1, tb, cnt);
@@ -951,7 +985,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
             const int y = f2i(ly * (float)p.hdr_h);
             const int val = (int)((uint32_t)x + (uint32_t)y * p.hdr_w);
             const int addr = (int)clampi(val, 0, (int)(p.hdr_w * p.hdr_h - 1u));
-            if (COUNT) cnt.hdr++;
+            if (COUNT) { cnt.hdr++; cnt.ld128++; }
             ps.accum = add4(ps.accum, mul4(mul4s(ps.mask, 2.f), p.hdr[addr]));
             ps.accum.w = ps.depth;
             out = ps.accum;
@@ -977,15 +1011,26 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
             cnt.attr += 24 + 48;
             cnt.mesh_hits++;
             const bool vb = HAS(F_VIEW_BRDF);
-            cnt.tex += (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb);
+            const uint32_t nt = (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb);
+            cnt.tex += nt;
+            cnt.ld128 += nt;
+            // the kernel specialised on the scene's features loads the uvs
+            // only when a texture is bound and the tangents only for a normal
+            // map or a BRDF (the generic kernel counting here loads both)
+            if ((p.flags & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u) cnt.ld64 += 3;
+            if ((p.flags & (F_TEX_NORM | F_BRDF)) != 0u) cnt.ld128 += 3;
             if (HAS(F_TEX_NORM) && dot4(h.tan, h.tan) > VR_EPS) {
                 cnt.attr += 48; cnt.tex++; cnt.nmap_hits++;
+                cnt.ld128 += 3 + 1;                            // normals + the normal-map texel
             } else if (!ref_alg<COUNT, FEAT>()) {
                 cnt.attr += 36;     // the face normal's vertices (the reference has them from its triangle test)
+                cnt.ld96 += 3;
             }
         } else if (hr.kind == HK_EXAMPLE) {
             const bool vb = HAS(F_VIEW_BRDF);
-            cnt.tex += (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb) + (HAS(F_TEX_NORM) != 0);
+            const uint32_t nt = (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb) + (HAS(F_TEX_NORM) != 0);
+            cnt.tex += nt;
+            cnt.ld128 += nt;
         }
     }
     if (ps.bounce == 0) {
@@ -1044,7 +1089,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
                                            mul4s(w, sqrt_exact(1 - rand2))));
         if HAS(F_BRDF) {
             const float dw = 24 * pow_p(newdir.x * newdir.x + newdir.y * newdir.y + newdir.z * newdir.z, -1.5f);
-            if (COUNT) cnt.brdf++;
+            if (COUNT) { cnt.brdf++; cnt.ld32 += 3; }
             const vr4 b = lookup_brdf(p.brdf, newdir, ray.d, h.n, h.tan);
             const vr4 bm = mk4(__builtin_fmaxf(b.x, 0.f), __builtin_fmaxf(b.y, 0.f), __builtin_fmaxf(b.z, 0.f),
                                __builtin_fmaxf(b.w, 0.f));
@@ -1463,6 +1508,7 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
         uint32_t s2 = y * p.times[f];
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
         path_begin(ps, s1, s2);
+        if (CNT) cnt.ld128 += 2;
         const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
         hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
         hr.bv = b.x;

@@ -36,11 +36,11 @@ constexpr int kMaxFramesPerLaunch = 64;
 // lookups.  The instrumented production kernels also fill slots
 // [kExecCounterBase, +kExecCounters): node visits served from the LDS copy,
 // triangle loads issued (36 B each), mesh hits shaded, mesh hits shaded
-// through the normal map, 16-B and 8-B lane loads of node visits served from
-// memory.  Slots 8..13 hold diagnostic-build phase timers.
+// through the normal map, and every global lane load issued, by width: 16, 12,
+// 8 and 4 B.  Slots 8..13 hold diagnostic-build phase timers.
 constexpr int kCounters = 8;
 constexpr int kExecCounterBase = 16;
-constexpr int kExecCounters = 6;
+constexpr int kExecCounters = 8;
 constexpr int kWaveTimesBase = 32;   // -DVR_WAVE_TIMES diagnostic builds: per-wave records from here
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles

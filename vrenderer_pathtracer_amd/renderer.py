@@ -366,12 +366,12 @@ class VRendererHIP:
             arr = (ctypes.c_uint32 * frames)(*[int(t) & 0xFFFFFFFF for t in times])
         if time_seed is None:
             time_seed = self.default_time if self.default_time is not None else int(_time.time() * 1000)
-        c = (ctypes.c_uint64 * 14)()
+        c = (ctypes.c_uint64 * 16)()
         check(self._lib.vrhip_render_profiled(self._need_ctx(), frames, arr, int(time_seed) & 0xFFFFFFFF, c),
               "vrhip_render_profiled")
         names = ["rays", "node_visits", "slot_reads", "tri_tests", "attr_bytes", "tex_fetches", "hdr_fetches",
-                 "brdf_fetches", "node_visits_lds", "tri_loads", "mesh_hits", "nmap_hits", "node_lane_loads_b128",
-                 "node_lane_loads_b64"]
+                 "brdf_fetches", "node_visits_lds", "tri_loads", "mesh_hits", "nmap_hits", "lane_loads_b128",
+                 "lane_loads_b96", "lane_loads_b64", "lane_loads_b32"]
         return {n: int(v) for n, v in zip(names, c)}
 
     def kernel_stats(self, reset: bool = False):
