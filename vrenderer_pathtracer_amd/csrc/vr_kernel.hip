@@ -528,6 +528,71 @@ __device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, 
     tr.tcur = SC ? (n == 0 ? ttop : key[0]) : 0.f;
 }
 
+// One visit of a quantized 4-wide node (F_Q4): three 16-B loads, the four
+// child boxes decoded as origin + q * 2^e per axis (one byte-to-float convert
+// and one FMA per bound, the slab distance directly: q * (s / d) + (origin -
+// o) / d), the entered children ordered by entry distance, the nearest next
+// and the others pushed far to near (at most 3 per level: the kQ4Stack class).
+template <bool COUNT, uint32_t FEAT, bool SC>
+__device__ __forceinline__ void node_stepQ4(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
+{
+    int* stk = L.stk;
+    if (COUNT) { cnt.nodes++; cnt.ld128 += 3; }
+    VR_LANE(0, 1);
+    const __amdgpu_buffer_rsrc_t qb = buf_rsrc(p.bvhq, p.n_nodesq * 48u);
+    const int off = tr.nodeAddr * 48;
+    const vr_u32x4 w0 = __builtin_amdgcn_raw_buffer_load_b128(qb, off, 0, 0);
+    const vr_u32x4 w1 = __builtin_amdgcn_raw_buffer_load_b128(qb, off + 16, 0, 0);
+    const vr_u32x4 w2 = __builtin_amdgcn_raw_buffer_load_b128(qb, off + 32, 0, 0);
+    auto h2f = [](uint32_t h) { return __half2float(__ushort_as_half((unsigned short)(h & 0xffffu))); };
+    const float ox = h2f(w0.x), oy = h2f(w0.x >> 16), oz = h2f(w0.y);
+    const float sx = __uint_as_float((((w0.y >> 16) & 31u) + p.q4_ebias) << 23);
+    const float sy = __uint_as_float((((w0.y >> 21) & 31u) + p.q4_ebias) << 23);
+    const float sz = __uint_as_float((((w0.y >> 26) & 31u) + p.q4_ebias) << 23);
+    const float ax = sx * tr.ivx, ay = sy * tr.ivy, az = sz * tr.ivz;   // exact: powers of two
+    const float bx = __builtin_fmaf(ox, tr.ivx, -tr.odx);
+    const float by = __builtin_fmaf(oy, tr.ivy, -tr.ody);
+    const float bz = __builtin_fmaf(oz, tr.ivz, -tr.odz);
+    float key[4];
+    int val[4];
+    auto child = [&](int i, int idx) {
+        const uint32_t sh = 8u * (uint32_t)i;
+        auto q = [&](uint32_t w) { return (float)((w >> sh) & 0xffu); };   // v_cvt_f32_ubyteN
+        const float a0 = __builtin_fmaf(q(w0.z), ax, bx), a1 = __builtin_fmaf(q(w0.w), ax, bx);
+        const float b0 = __builtin_fmaf(q(w1.x), ay, by), b1 = __builtin_fmaf(q(w1.y), ay, by);
+        const float c0 = __builtin_fmaf(q(w1.z), az, bz), c1 = __builtin_fmaf(q(w1.w), az, bz);
+        const float tmin = span_begin(a0, a1, b0, b1, c0, c1, 0.0f);
+        const float tmax = span_end(a0, a1, b0, b1, c0, c1, 1e20f);
+        const bool hit = (tmax >= tmin) && (tmin <= tr.tcull) && (idx != kSentinel);
+        key[i] = hit ? tmin : __builtin_inff();
+        val[i] = idx;
+    };
+    child(0, (int)w2.x);
+    child(1, (int)w2.y);
+    child(2, (int)w2.z);
+    child(3, (int)w2.w);
+    const int n = (key[0] != __builtin_inff()) + (key[1] != __builtin_inff()) + (key[2] != __builtin_inff()) +
+                  (key[3] != __builtin_inff());
+    auto cs = [&](int i, int j) {                          // compare-swap, ties keep slot order
+        const bool sw = key[j] < key[i];
+        const float ki = key[i], kj = key[j];
+        const int vi = val[i], vj = val[j];
+        key[i] = sw ? kj : ki; key[j] = sw ? ki : kj;
+        val[i] = sw ? vj : vi; val[j] = sw ? vi : vj;
+    };
+    cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+    const int top = stk[tr.sp * L.stride];
+    if (n >= 4) stk[(tr.sp + 1) * L.stride] = val[3];
+    tr.sp += n >= 4 ? 1 : 0;
+    if (n >= 3) stk[(tr.sp + 1) * L.stride] = val[2];
+    tr.sp += n >= 3 ? 1 : 0;
+    if (n >= 2) stk[(tr.sp + 1) * L.stride] = val[1];
+    tr.sp += n >= 2 ? 1 : (n == 0 ? -1 : 0);
+    tr.nodeAddr = n == 0 ? top : val[0];
+    tr.tcur = 0.f;
+    (void)SC;
+}
+
 // Equal-t tie-break of the culled traversal.  The reference keeps the first
 // of two triangles hit at exactly the same distance (strict `<`,
 // PathTracer.cu:379), i.e. the one its depth-first walk tests first: slot
@@ -650,7 +715,8 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
     int leafAddr = 0;
     float leafT = 0.f;                                          // slab entry of the postponed leaf
     while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
-        if (HAS(F_WIDE)) node_step4<COUNT, FEAT, SC>(p, r, tr, L, cnt);
+        if (HAS(F_Q4)) node_stepQ4<COUNT, FEAT, SC>(p, r, tr, L, cnt);
+        else if (HAS(F_WIDE)) node_step4<COUNT, FEAT, SC>(p, r, tr, L, cnt);
         else node_step<COUNT, FEAT, SC>(p, r, tr, L, cnt);
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
             leafAddr = tr.nodeAddr;
@@ -1399,14 +1465,14 @@ enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3 };
 #endif
 static_assert(VR_PATH_BLOCK % kBlockThreads == 0, "VR_PATH_BLOCK must be a multiple of 256");
 static_assert((4 * VR_PATH_WAVES * 64) % VR_PATH_BLOCK == 0, "whole blocks per CU");
-constexpr int wave_block(int stack) { return stack <= 24 ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads; }
+constexpr int wave_block(int stack) { return stack <= kQ4Stack ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads; }
 // Launches of fewer than 2^24 paths (sharded frames, RenderParams::small_blocks)
 // take 256-thread blocks at the same residency: a block frees its CU slot once
 // its 4 waves are done rather than 12, so the launch's drain overlaps the next
 // launch sooner.  Projected 8-rank C2 step 1.283 -> 1.193 ms (C3 0.468 ->
 // 0.420 ms), while whole frames keep the 768-thread blocks (C2 3,437 vs 3,244).
-constexpr int wave_block_small(int stack) { return stack <= 24 ? kBlockThreads : wave_block(stack); }
-constexpr int path_waves(int stack) { return stack <= 24 ? VR_PATH_WAVES : stack <= 32 ? 4 : 2; }
+constexpr int wave_block_small(int stack) { return stack <= kQ4Stack ? kBlockThreads : wave_block(stack); }
+constexpr int path_waves(int stack) { return stack <= kQ4Stack ? VR_PATH_WAVES : stack <= 32 ? 4 : 2; }
 constexpr int path_blocks_per_cu(int stack, int bt) { return 4 * path_waves(stack) * 64 / bt; }
 // LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
 // the node cache takes what the stacks leave (56 B per node)
@@ -1678,8 +1744,13 @@ constexpr uint32_t kWide = F_WIDE;
 #else
 constexpr uint32_t kWide = 0u;
 #endif
+#ifdef VR_Q4
+constexpr uint32_t kQ4 = F_Q4;
+#else
+constexpr uint32_t kQ4 = 0u;
+#endif
 constexpr uint32_t kFeatAll =
-    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT | kWide;
+    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT | kWide | kQ4;
 static_assert((kFeatAll & F_COUNT_EXEC) == 0u, "F_COUNT_EXEC is a compile-time kernel variant, not a scene flag");
 constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH;                                  // C2
 constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                              // C1
@@ -1719,6 +1790,10 @@ static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth
     const uint32_t blocks = n_tiles * p.split;
     if (!wave)
         hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+#ifdef VR_Q4
+    else if ((p.flags & F_Q4) != 0u)
+        launch_wave<kQ4Stack, FEAT | F_Q4>(p, n_tiles, s);
+#endif
     else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
         launch_wave<16, FEAT>(p, n_tiles, s);
     else if (stack_depth <= 24 && VR_MIN_SPEC_STACK <= 24)
@@ -1734,6 +1809,10 @@ static void launch_exec_counted(const RenderParams& p, uint32_t n_tiles, int sta
     constexpr uint32_t FE = kFeatAll | F_COUNT_EXEC;
     if ((p.flags & F_MESH) == 0u)
         hipLaunchKernelGGL((render_kernel<16, true, FE>), dim3(n_tiles * p.split), dim3(kBlockThreads), 0, s, p);
+#ifdef VR_Q4
+    else if ((p.flags & F_Q4) != 0u)
+        launch_wave<kQ4Stack, FE>(p, n_tiles, s);
+#endif
     else if (stack_depth <= 16)
         launch_wave<16, FE>(p, n_tiles, s);
     else if (stack_depth <= 24)
@@ -1748,7 +1827,7 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int 
 {
     if (n_tiles == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    const uint32_t need = p.flags & kFeatAll;
+    const uint32_t need = p.flags & kFeatAll & ~kQ4;      // F_Q4 picks the walk inside launch_spec
     const uint32_t blocks = n_tiles * p.split;   // split == 1 for the counting variant
     if (count == 2) {
         launch_exec_counted(p, n_tiles, stack_depth, s);

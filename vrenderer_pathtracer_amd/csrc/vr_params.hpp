@@ -28,7 +28,9 @@ enum Flags : uint32_t {
     // launch shape and results, plus per-lane counts of the memory operations
     // they execute
     F_COUNT_EXEC = 1u << 10,
+    F_Q4 = 1u << 11,         // culled traversal over the quantized 4-wide nodes (bvhq)
 };
+constexpr int kQ4Stack = 26;         // stack class of the quantized 4-wide walk: 3 pushes per level, depth <= 8
 
 constexpr int kMaxFramesPerLaunch = 64;
 // counting variants, slots [0, kCounters): rays, node visits, vert0 slot
@@ -81,6 +83,9 @@ struct RenderParams {
     const vr4* bvh4;                 // 4-wide nodes, 7 rows each (culled traversal, VR_BVH4)
     uint32_t n_nodes4;
     const vr4* bvh16;                // same nodes, conservative fp16 boxes, 32 B each (culled traversal)
+    const uint32_t* bvhq;            // quantized 4-wide nodes, 48 B each (F_Q4; vrhip_api.cpp build_nodes_q4)
+    uint32_t n_nodesq;
+    uint32_t q4_ebias;               // biased IEEE exponent of a stored scale exponent 0
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
     const vr3* verts;                // 3 vertices per triangle, compact leaf order (face normal at shading)
     const vr3* tri_e;                // per triangle (v0, v1 - v0, v2 - v0): the traversal's copy

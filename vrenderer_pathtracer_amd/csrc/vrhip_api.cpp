@@ -71,9 +71,10 @@ struct vrhip_ctx {
     bool cornell = false, example = false, view_brdf = false;
     bool strict = false;          // exact reference traversal (no t-culling)
     // mesh
-    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr4* bvh4 = nullptr; vr3* verts = nullptr; vr3* tri_e = nullptr; unsigned long long* tpath = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
+    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr4* bvh4 = nullptr; uint32_t* bvhq = nullptr; vr3* verts = nullptr; vr3* tri_e = nullptr; unsigned long long* tpath = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
     uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0, dev_nodes4 = 0;
+    uint32_t dev_nodesq = 0, q4_depth = 0, q4_ebias = 0;    // quantized 4-wide nodes (0 nodes: not built)
     bool mesh = false;
     // environment / textures / brdf
     vr4* hdr = nullptr; uint32_t hdr_w = 0, hdr_h = 0;
@@ -160,6 +161,8 @@ struct DeviceMesh {
     std::vector<vr4> nodes, normals, tangents;
     std::vector<vr4> nodes16;        // 2 x 16 B per node: conservative fp16 boxes + child indices
     std::vector<vr4> nodes4;         // 4-wide nodes, 7 x 16 B each (collapsed binary tree)
+    std::vector<uint32_t> nodesq;    // quantized 4-wide nodes, 12 dwords (48 B) each
+    uint32_t q4_depth = 0, q4_ebias = 0;
     std::vector<vr3> tris;           // packed 12 B vertices (vertex .w never reaches a result)
     std::vector<vr3> tri_e;          // per triangle v0, v1 - v0, v2 - v0 (fp32, the kernel's own subtractions)
     std::vector<unsigned long long> tpath;   // per triangle: leaf path from the root under a leading 1 bit
@@ -399,6 +402,123 @@ void build_nodes4(DeviceMesh& dm)
     }
 }
 
+// Quantized 4-wide nodes for the t-culled traversal (default where the stack
+// fits, see render_impl): each node holds the grandchildren of one binary node
+// (a leaf child is kept as is), so a ray visits about half as many nodes, and
+// a node is 48 B -- three 16-B loads:
+//   dword 0: origin.x | origin.y << 16 (IEEE halves, rounded down)
+//   dword 1: origin.z | ex << 16 | ey << 21 | ez << 26 (5-bit scale exponents)
+//   dwords 2..7: lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4] (bytes)
+//   dwords 8..11: child[4]: >= 0 quantized-node index, < 0 leaf code, or the
+//                 traversal's sentinel for an empty slot (never entered).
+// A child box is [origin + lo * s, origin + hi * s] per axis with
+// s = 2^(e + ebias - 127): lows rounded down and highs up, so it contains the
+// exact box and no hit is lost (the equal-t tie-break keeps the result
+// independent of the changed visit order).  ebias is chosen per mesh so that
+// the largest node's exponent is representable; the smallest nodes may get a
+// coarser (still conservative) scale.
+void build_nodes_q4(DeviceMesh& dm)
+{
+    dm.nodesq.clear();
+    dm.q4_depth = 0;
+    const size_t n = dm.nodes.size() / 4;
+    if (n == 0) return;
+    struct Child { float lo[3], hi[3]; int32_t idx; };
+    auto bin_child = [&](size_t node, int ch) {
+        Child c;
+        const vr4 a = dm.nodes[4 * node + ch], z = dm.nodes[4 * node + 2], ni = dm.nodes[4 * node + 3];
+        c.lo[0] = a.x; c.hi[0] = a.y; c.lo[1] = a.z; c.hi[1] = a.w;
+        c.lo[2] = ch ? z.z : z.x; c.hi[2] = ch ? z.w : z.y;
+        std::memcpy(&c.idx, ch ? &ni.y : &ni.x, 4);
+        return c;
+    };
+    auto half_to_float = [](uint16_t h) {
+        const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+        double f = e == 0 ? std::ldexp((double)m, -24) : (e == 31 ? INFINITY : std::ldexp((double)(m | 0x400u), (int)e - 25));
+        return (h & 0x8000u) ? -f : f;
+    };
+    std::vector<int32_t> qid(n, -1);                 // binary node -> quantized-node index
+    std::vector<size_t> queue{ 0 };
+    std::vector<uint32_t> qdepth{ 1 };
+    qid[0] = 0;
+    std::vector<std::array<Child, 4>> kids;
+    std::vector<int> nkids;
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        std::array<Child, 4> k4;
+        int nk = 0;
+        for (int ch = 0; ch < 2; ++ch) {
+            const Child c = bin_child(queue[qi], ch);
+            if (c.idx >= 0) { k4[nk++] = bin_child((size_t)c.idx / 4, 0); k4[nk++] = bin_child((size_t)c.idx / 4, 1); }
+            else k4[nk++] = c;
+        }
+        for (int k = 0; k < nk; ++k) {
+            if (k4[k].idx < 0) continue;
+            const size_t cb = (size_t)k4[k].idx / 4;
+            if (qid[cb] < 0) { qid[cb] = (int32_t)queue.size(); queue.push_back(cb); qdepth.push_back(qdepth[qi] + 1); }
+        }
+        kids.push_back(k4);
+        nkids.push_back(nk);
+        dm.q4_depth = std::max(dm.q4_depth, qdepth[qi]);
+    }
+    // origins (fp16, rounded down) and the smallest scale exponent per axis
+    const size_t nq = queue.size();
+    std::vector<std::array<uint16_t, 3>> org(nq);
+    std::vector<std::array<int, 3>> expo(nq);
+    int max_e = -126;
+    for (size_t i = 0; i < nq; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (int k = 0; k < nkids[i]; ++k) { lo = std::min(lo, kids[i][k].lo[a]); hi = std::max(hi, kids[i][k].hi[a]); }
+            org[i][a] = half_bits_directed(lo, false);
+            if (!(std::fabs(lo) < 60000.f) || !(std::fabs(hi) < 60000.f)) {   // beyond fp16 origins: binary nodes only
+                dm.nodesq.clear();
+                dm.q4_depth = 0;
+                return;
+            }
+            const double ext = (double)hi - half_to_float(org[i][a]);
+            int e = -126;
+            if (ext > 0.0) {
+                e = (int)std::ceil(std::log2(ext / 255.0));
+                while (std::ldexp(255.0, e) < ext) ++e;
+                while (e > -126 && std::ldexp(255.0, e - 1) >= ext) --e;
+            }
+            expo[i][a] = std::max(e, -126);
+            max_e = std::max(max_e, expo[i][a]);
+        }
+    }
+    const int ebias = std::max(max_e - 31, -126) + 127;   // biased IEEE exponent of stored exponent 0
+    dm.q4_ebias = (uint32_t)ebias;
+    dm.nodesq.assign(12 * nq, 0u);
+    for (size_t i = 0; i < nq; ++i) {
+        uint32_t* w = &dm.nodesq[12 * i];
+        int d[3];
+        double origin[3], scale[3];
+        for (int a = 0; a < 3; ++a) {
+            d[a] = std::max(expo[i][a] + 127 - ebias, 0);          // coarser for the very smallest nodes
+            origin[a] = half_to_float(org[i][a]);
+            scale[a] = std::ldexp(1.0, d[a] + ebias - 127);
+        }
+        w[0] = (uint32_t)org[i][0] | ((uint32_t)org[i][1] << 16);
+        w[1] = (uint32_t)org[i][2] | ((uint32_t)d[0] << 16) | ((uint32_t)d[1] << 21) | ((uint32_t)d[2] << 26);
+        for (int k = 0; k < 4; ++k) {
+            int32_t idx = 0x76543210;                               // empty slot: the sentinel
+            if (k < nkids[i]) {
+                const Child& c = kids[i][k];
+                idx = c.idx >= 0 ? qid[(size_t)c.idx / 4] : c.idx;
+                for (int a = 0; a < 3; ++a) {
+                    const double ql = std::floor(((double)c.lo[a] - origin[a]) / scale[a]);
+                    const double qh = std::ceil(((double)c.hi[a] - origin[a]) / scale[a]);
+                    const uint32_t bl = (uint32_t)std::min(std::max(ql, 0.0), 255.0);
+                    const uint32_t bh = (uint32_t)std::min(std::max(qh, 0.0), 255.0);
+                    w[2 + 2 * a] |= bl << (8 * k);
+                    w[3 + 2 * a] |= bh << (8 * k);
+                }
+            }
+            std::memcpy(&w[8 + k], &idx, 4);
+        }
+    }
+}
+
 bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const vr4* normals,
                       const vr4* tangents, const vr2* uvs, DeviceMesh& dm, std::string& why)
 {
@@ -450,6 +570,7 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
 #endif
     build_nodes16(dm);
     build_nodes4(dm);
+    build_nodes_q4(dm);
     if (dm.tris.empty()) {
         dm.tris.push_back(vr3{ 0, 0, 0 });
         dm.normals.push_back(vr4{ 0, 0, 0, 0 });
@@ -558,7 +679,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     quiesce(c);
     dfree(c->accum); dfree(c->rgba); dfree(c->depth);
-    dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->verts); dfree(c->tri_e); dfree(c->tpath); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
+    dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->bvhq); dfree(c->verts); dfree(c->tri_e); dfree(c->tpath); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     for (int i = 0; i < 2; ++i)
         if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
@@ -642,6 +763,9 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     if ((rc = upload(c, c->bvh16, dm.nodes16.data(), dm.nodes16.size() * 16))) return rc;
     if ((rc = upload(c, c->bvh4, dm.nodes4.data(), dm.nodes4.size() * 16))) return rc;
     c->dev_nodes4 = (uint32_t)(dm.nodes4.size() / 7);
+    if ((rc = upload(c, c->bvhq, dm.nodesq.data(), dm.nodesq.size() * 4))) return rc;
+    c->dev_nodesq = (uint32_t)(dm.nodesq.size() / 12);
+    c->q4_depth = dm.q4_depth; c->q4_ebias = dm.q4_ebias;
     if ((rc = upload(c, c->verts, dm.tris.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->tri_e, dm.tri_e.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->tpath, dm.tpath.data(), dm.tpath.size() * sizeof(unsigned long long)))) return rc;
@@ -910,6 +1034,12 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     if (!c->strict && c->mesh && c->bvh_depth <= 30) f |= vr::F_WIDE;   // <= 3 pushes per 4-wide level
 #endif
     if (c->mesh) f |= vr::F_MESH;
+#ifdef VR_Q4
+    // quantized 4-wide walk (opt-in: 43 % fewer node visits and 9 % fewer lane
+    // loads on C2, but 11 % slower -- DESIGN.md); <= 3 pushes per level in kQ4Stack
+    if (!c->strict && c->mesh && c->dev_nodesq > 0 && 3 * c->q4_depth + 1 <= (uint32_t)vr::kQ4Stack)
+        f |= vr::F_Q4;
+#endif
     if (c->brdf) f |= vr::F_BRDF;
     if (c->tex[0]) f |= vr::F_TEX_DIFF;
     if (c->tex[1]) f |= vr::F_TEX_NORM;
@@ -918,6 +1048,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.tiles_x = p.wr / 16u;
     p.rank = c->rank; p.nranks = c->nranks;
     p.bvh4 = c->bvh4; p.n_nodes4 = c->mesh ? c->dev_nodes4 : 0;
+    p.bvhq = c->bvhq; p.n_nodesq = c->mesh ? c->dev_nodesq : 0; p.q4_ebias = c->q4_ebias;
     p.bvh = c->bvh; p.bvh16 = c->bvh16; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.tri_e = c->tri_e; p.tpath = c->tpath; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
     p.hdr = c->hdr; p.hdr_w = c->hdr_w; p.hdr_h = c->hdr_h;
     for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
