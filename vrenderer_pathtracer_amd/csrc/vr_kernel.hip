@@ -266,6 +266,7 @@ constexpr bool kFp16Nodes = false;
 
 struct Lds {
     int* stk;                 // this thread's column of the stack
+    unsigned short* stk16;    // F_LDS_TREE: 16-bit entries, (parent node << 1) | child slot; 0xffff = sentinel
     unsigned short* tstk;     // entry distance of each stacked child (bf16, rounded down)
     const vr4* nodes;         // fp32 nodes: 3 rows per cached node; fp16 nodes: 2 rows per node
     const int2* idx;          // fp32 nodes: child indices per cached node
@@ -298,7 +299,8 @@ template <uint32_t FEAT, bool SC>
 __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, float t0, Trav& tr, const Lds& L)
 {
     tr.sp = 0;
-    L.stk[0] = kSentinel;
+    if (HAS(F_LDS_TREE)) L.stk16[0] = 0xffffu;
+    else L.stk[0] = kSentinel;
     if (SC) L.tstk[0] = 0;
     tr.nodeAddr = 0;
     tr.tcur = 0.f;
@@ -340,6 +342,24 @@ __device__ __forceinline__ int trav_pop(Trav& tr, const Lds& L)
     return L.stk[i];
 }
 
+// F_LDS_TREE: a stack entry names the pushed child by its parent and slot;
+// the child reference is read back from the parent's LDS row (ds_read_b32)
+__device__ __forceinline__ int lt_ref(const Lds& L, uint32_t e)
+{
+    if (e == 0xffffu) return kSentinel;
+    return __float_as_int(reinterpret_cast<const float*>(L.nodes + 2u * (e >> 1) + 1u)[2u + (e & 1u)]);
+}
+template <uint32_t FEAT, bool SC>
+__device__ __forceinline__ int trav_pop_f(const RenderParams& p, Trav& tr, const Lds& L)
+{
+    if (HAS(F_LDS_TREE)) {
+        const int i = (tr.sp--) * L.stride;
+        tr.tcur = 0.f;
+        return lt_ref(L, L.stk16[i]);
+    }
+    return trav_pop<SC>(tr, L);
+}
+
 // One inner-node visit (:295-343): fetch (LDS copy or L2/HBM), two slab
 // tests, near child next, far child pushed when both are entered, pop when
 // neither is.  Leaves in tr.nodeAddr are left to the caller.
@@ -367,7 +387,8 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
 #else
     const bool in_lds = __ballot(!dead && node >= L.n_cached) == 0ull;
 #endif
-    if (COUNT && !dead) {
+    if (COUNT && !dead && HAS(F_LDS_TREE)) cnt.nodes_lds++;
+    else if (COUNT && !dead) {
         cnt.nodes_lds += in_lds ? 1u : 0u;
         if (!in_lds) { cnt.ld128 += (kFp16Nodes && !strict) ? 2u : 3u; cnt.ld64 += (kFp16Nodes && !strict) ? 0u : 1u; }
     }
@@ -377,7 +398,10 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
         // fetches per node instead of four; a box can only grow, so no hit
         // the exact box admits is lost
         vr4 a, b;
-        if (in_lds) {
+        if (HAS(F_LDS_TREE)) {                          // the whole tree is in LDS: two ds_read_b128
+            a = L.nodes[2 * node];
+            b = L.nodes[2 * node + 1];
+        } else if (in_lds) {
             a = L.nodes[2 * node];
             b = L.nodes[2 * node + 1];
         } else {
@@ -460,6 +484,14 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
         cnt.tm[1] += ns2 - ns1;
     }
 #endif
+    if (HAS(F_LDS_TREE)) {
+        const uint32_t etop = L.stk16[tr.sp * L.stride];
+        if (both) L.stk16[(tr.sp + 1) * L.stride] = (unsigned short)(((uint32_t)node << 1) | (swp ? 0u : 1u));
+        tr.sp += both ? 1 : (none ? -1 : 0);
+        tr.nodeAddr = none ? lt_ref(L, etop) : nearc;
+        tr.tcur = 0.f;
+        return;
+    }
     const int top = stk[tr.sp * L.stride];
     const float ttop = SC ? tkey_f(L.tstk[tr.sp * L.stride]) : 0.f;
     if (both) {
@@ -721,7 +753,7 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
             leafAddr = tr.nodeAddr;
             leafT = tr.tcur;
-            tr.nodeAddr = trav_pop<SC>(tr, L);
+            tr.nodeAddr = trav_pop_f<FEAT, SC>(p, tr, L);
         }
         // the wave moves on to the leaves once (nearly) every lane holds one;
         // lanes still searching resume in the next outer iteration
@@ -771,7 +803,7 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
 #endif
         leafAddr = tr.nodeAddr;
         leafT = tr.tcur;
-        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop<SC>(tr, L);
+        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop_f<FEAT, SC>(p, tr, L);
     }
 }
 
@@ -1486,6 +1518,9 @@ constexpr int path_cache_nodes(int stack, int bt) {
 #endif
 
 template <int STACK, uint32_t FEAT, int BT>
+__device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L);
+
+template <int STACK, uint32_t FEAT, int BT>
 __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(const RenderParams p)
 {
     constexpr int CN = path_cache_nodes(STACK, BT);
@@ -1493,8 +1528,38 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
     __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * BT : 1];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
-    const int tid = threadIdx.x;
-    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, tid);
+    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, (int)threadIdx.x);
+    wave_body<STACK, FEAT, BT>(p, L);
+}
+
+// F_LDS_TREE: the same path kernel with the whole conservative-fp16 tree
+// copied into each block's LDS (dynamic, 32 B per node) and 16-bit stack
+// entries, one 1,024-thread block per CU (4 waves per SIMD): every node visit
+// is two ds_read_b128 instead of two vector-memory loads, which is what the
+// texture path spends most of its time on (profiles/r02_c2_mem.md).
+template <uint32_t FEAT>
+__global__ void __launch_bounds__(kLdsTreeBlock, 4) render_wave_kernel_lt(const RenderParams p)
+{
+    __shared__ unsigned short lds_stk16[kLdsTreeStack * kLdsTreeBlock];
+    extern __shared__ vr4 lds_tree[];
+    const int tid = (int)threadIdx.x;
+    for (uint32_t i = (uint32_t)tid; i < 2u * p.n_nodes; i += (uint32_t)kLdsTreeBlock) lds_tree[i] = p.bvh16[i];
+    __syncthreads();
+    Lds L;
+    L.stk = nullptr;
+    L.stk16 = lds_stk16 + tid;
+    L.tstk = nullptr;
+    L.stride = kLdsTreeBlock;
+    L.nodes = lds_tree;
+    L.idx = nullptr;
+    L.n_cached = (int)p.n_nodes;
+    wave_body<kLdsTreeStack, FEAT, kLdsTreeBlock>(p, L);
+}
+
+template <int STACK, uint32_t FEAT, int BT>
+__device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
+{
+    const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
     const uint32_t n_paths = 2u * p.n_frames;
     const uint32_t n_sub = p.path_stride >> 6;             // 8x8 sub-tiles of the rank's tiles
@@ -1561,7 +1626,17 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
     Trav tr;
     auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
         if (sub == ~0u) { state = LS_DONE; return; }
+#ifdef VR_PIXEL_MAJOR
+        // the sub-tile's items pixel-major: a chunk holds all paths of
+        // 64 / n_paths pixels, so a wave's bounce rays share their origins
+        {
+            const uint32_t e = path * 64u + px;
+            q = e % n_paths;
+            px = e / n_paths;
+        }
+#else
         q = path;
+#endif
         slot = sub * 64u + px;
         const uint32_t f = q >> 1;
         const uint32_t tile = sub >> 2, quad = sub & 3u;
@@ -1774,6 +1849,23 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
                        dim3(BT), 0, s, p);
 }
 
+// F_LDS_TREE launch: the primary pass reads the tree from memory; the path
+// kernel copies it into LDS (the host checks it fits next to the stacks)
+template <uint32_t FEAT>
+static void launch_wave_lt(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
+{
+    hipLaunchKernelGGL((primary_kernel<kLdsTreeStack, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    const size_t dyn = (size_t)p.n_nodes * 32u;
+    static bool attr_set = false;                       // > 64 KB of dynamic LDS: raise the limit once
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&render_wave_kernel_lt<FEAT | F_LDS_TREE>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kLdsBytesPerCU - kLdsTreeStack * kLdsTreeBlock * 2);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((render_wave_kernel_lt<FEAT | F_LDS_TREE>), dim3(p.wave_blocks), dim3(kLdsTreeBlock), dyn, s, p);
+}
+
 template <uint32_t FEAT>
 static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
 {
@@ -1794,6 +1886,8 @@ static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth
     else if ((p.flags & F_Q4) != 0u)
         launch_wave<kQ4Stack, FEAT | F_Q4>(p, n_tiles, s);
 #endif
+    else if ((p.flags & F_LDS_TREE) != 0u)
+        launch_wave_lt<FEAT>(p, n_tiles, s);
     else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
         launch_wave<16, FEAT>(p, n_tiles, s);
     else if (stack_depth <= 24 && VR_MIN_SPEC_STACK <= 24)
@@ -1813,6 +1907,8 @@ static void launch_exec_counted(const RenderParams& p, uint32_t n_tiles, int sta
     else if ((p.flags & F_Q4) != 0u)
         launch_wave<kQ4Stack, FE>(p, n_tiles, s);
 #endif
+    else if ((p.flags & F_LDS_TREE) != 0u)
+        launch_wave_lt<FE>(p, n_tiles, s);
     else if (stack_depth <= 16)
         launch_wave<16, FE>(p, n_tiles, s);
     else if (stack_depth <= 24)

@@ -29,7 +29,13 @@ enum Flags : uint32_t {
     // they execute
     F_COUNT_EXEC = 1u << 10,
     F_Q4 = 1u << 11,         // culled traversal over the quantized 4-wide nodes (bvhq)
+    F_LDS_TREE = 1u << 12,   // culled traversal with the whole fp16 tree in each block's LDS
 };
+// LDS-resident tree walk: one 1024-thread block per CU (4 waves/SIMD), the
+// fp16 tree (32 B per node) in dynamic LDS next to 16-bit stacks of kLdsTreeStack entries
+constexpr int kLdsTreeBlock = 1024;
+constexpr int kLdsTreeStack = 16;
+constexpr int kLdsBytesPerCU = 163840;
 constexpr int kQ4Stack = 26;         // stack class of the quantized 4-wide walk: 3 pushes per level, depth <= 8
 
 constexpr int kMaxFramesPerLaunch = 64;

@@ -1034,6 +1034,14 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     if (!c->strict && c->mesh && c->bvh_depth <= 30) f |= vr::F_WIDE;   // <= 3 pushes per 4-wide level
 #endif
     if (c->mesh) f |= vr::F_MESH;
+#ifdef VR_LDS_TREE
+    // opt-in (C2 -19 %, C3 -11 % at 4 waves/SIMD: DESIGN.md): the whole conservative-fp16 tree in each path-kernel block's LDS when it
+    // fits next to the 16-bit stacks of a 1,024-thread block (the 10k-triangle
+    // knot: 3,724 nodes x 32 B = 119 KB); depth <= 15 for the 16-entry stacks
+    if (!c->strict && c->mesh && c->bvh_depth <= 15 &&
+        (size_t)c->dev_nodes * 32u + (size_t)vr::kLdsTreeStack * vr::kLdsTreeBlock * 2u + 1024u <= (size_t)vr::kLdsBytesPerCU)
+        f |= vr::F_LDS_TREE;
+#endif
 #ifdef VR_Q4
     // quantized 4-wide walk (opt-in: 43 % fewer node visits and 9 % fewer lane
     // loads on C2, but 11 % slower -- DESIGN.md); <= 3 pushes per level in kQ4Stack
