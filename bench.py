@@ -19,8 +19,12 @@ this process starts `torch.distributed.run` with N ranks as a CHILD process
 (it never touches the GPU itself) and exits with the child's status.  16x16
 pixel tiles are dealt round-robin; each rank renders its tiles of every frame,
 then one RCCL gather (ncclGather through the library's C ABI,
-vrhip_comm_gather) brings the RGBA8 tiles to rank 0 per step.  Strong scaling:
-the frame size is fixed.
+vrhip_comm_gather) brings the RGBA8 tiles to rank 0 per step.  The frame size
+is fixed; a step accumulates 16 x N frames (every GPU renders the equivalent
+of 16 full 1280x720 frames per step and gather, as at N = 1: "weak" scaling
+in samples per step -- SURVEY.md 8e: several frames per gather so that the
+gather and each launch's drain stay small against the step).  --strong keeps
+16 frames per step for any N.
 
 Prints ONE JSON line (rank 0).  value = total paths of all ranks / max-over-
 ranks wall time of the K timed steps.  "interactive" = the same config one
@@ -186,7 +190,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames-per-step", type=int, default=16)
+    ap.add_argument("--frames-per-step", type=int, default=None,
+                    help="frames accumulated per step (= per gather); default 16 x N: every GPU renders 16 "
+                         "full-frame equivalents per step whatever N (weak scaling in samples, fixed resolution)")
+    ap.add_argument("--strong", action="store_true", help="16 frames per step for any N (strong scaling)")
     ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--interactive-frames", type=int, default=30,
@@ -243,7 +250,8 @@ def main():
     CFG = args.config
     scene = scenes.make_scene(CFG)
     W, H = scene["width"], scene["height"]
-    F = args.frames_per_step
+    F = args.frames_per_step or (16 if args.strong else 16 * world)
+    scaling = "strong" if (args.strong or (args.frames_per_step and world > 1)) else "weak"
 
     r = VRendererHIP(gpu)
     scenes.load_into(r, scene)
@@ -394,7 +402,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": WORKLOADS[CFG][1],

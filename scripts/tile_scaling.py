@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Projected strong scaling of the band sharding, measured on ONE GPU.
 
-  python scripts/tile_scaling.py [C2] [frames_per_step] [path_split, 0 = auto] [N list, e.g. 1,8]
+  python scripts/tile_scaling.py [C2] [frames_per_step | wF] [path_split, 0 = auto] [N list, e.g. 1,8]
+
+frames_per_step "w16" = 16 x N frames per step (bench.py's default: per-GPU
+work per step fixed); a number = that many frames for every N (strong).
 
 For N in 1, 2, 4, 8 this renders rank 0's share of an N-way band split (rank
 0 owns the most tiles) and reports the kernel time per step, the projected
@@ -20,17 +23,21 @@ import torch  # noqa: E402
 from vrenderer_pathtracer_amd import VRendererHIP, scenes  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
-F = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+FARG = sys.argv[2] if len(sys.argv) > 2 else "8"
+WEAK = FARG.startswith("w")
+F0 = int(FARG[1:] if WEAK else FARG)
 SPLIT = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 NS = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
 sc = scenes.make_scene(cfg)
 W, H = sc["width"], sc["height"]
-paths = (W // 16) * 16 * (H // 16) * 16 * 2 * F
+px = (W // 16) * 16 * (H // 16) * 16
 r = VRendererHIP(0)
 scenes.load_into(r, sc)
 r.set_path_split(SPLIT)
 base = None
 for n in NS:
+    F = F0 * n if WEAK else F0
+    paths = px * 2 * F
     r.set_tiling(0, n)
     r.clearBuffer()
     for i in range(2):
@@ -46,6 +53,6 @@ for n in NS:
     kms, launches = r.kernel_stats()
     rate = paths / dt / 1e6
     base = base or rate
-    print(f"{cfg} split={SPLIT} N={n}: rank-0 px {r.owned_pixels():7d}  step {dt * 1e3:8.3f} ms  kernel {kms / launches:8.3f} ms  "
+    print(f"{cfg} F={F} split={SPLIT} N={n}: rank-0 px {r.owned_pixels():7d}  step {dt * 1e3:8.3f} ms  kernel {kms / launches:8.3f} ms  "
           f"projected {rate:9.1f} Mpaths/s  eff {rate / (n * base):.3f}", flush=True)
 r.cleanUp()
