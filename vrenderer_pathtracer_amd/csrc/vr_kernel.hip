@@ -265,6 +265,7 @@ constexpr bool kFp16Nodes = false;
 #endif
 
 struct Lds {
+    vr4* stage;               // path kernel: this block's path-result staging rows (stage_slots)
     int* stk;                 // this thread's column of the stack
     unsigned short* stk16;    // F_LDS_TREE: 16-bit entries, (parent node << 1) | child slot; 0xffff = sentinel
     unsigned short* tstk;     // entry distance of each stacked child (bf16, rounded down)
@@ -1505,12 +1506,30 @@ constexpr int wave_block(int stack) { return stack <= kQ4Stack ? VR_PATH_BLOCK :
 // 0.420 ms), while whole frames keep the 768-thread blocks (C2 3,437 vs 3,244).
 constexpr int wave_block_small(int stack) { return stack <= kQ4Stack ? kBlockThreads : wave_block(stack); }
 constexpr int path_waves(int stack) { return stack <= kQ4Stack ? VR_PATH_WAVES : stack <= 32 ? 4 : 2; }
+// Path-result staging (opt-in, -DVR_STAGE_SLOTS=n): per wave, n rows of 64
+// results (1 KB each) in LDS, one per chunk in flight; a chunk's row is
+// written to the scratch with one coalesced store when its 64 paths have
+// ended, instead of scattered 16-B stores that leave lines partially written
+// in L2 (WRITE_SIZE 1.8x the result bytes on C2).  Measured: 2 slots C2 -3 %,
+// C3 -8 %, WRITE_SIZE 2.6x (the slot bookkeeping spills to scratch, and a
+// chunk finds no free slot while stragglers of older chunks hold both);
+// 3 slots 97 VGPRs, C2 -35 %, 1.6x.  Stack classes with room in LDS only.
+#ifndef VR_STAGE_SLOTS
+#define VR_STAGE_SLOTS 0
+#endif
+#ifdef VR_PIXEL_MAJOR
+constexpr int stage_slots(int stack) { return 0 * stack; }   // chunks are not contiguous result rows
+#else
+constexpr int stage_slots(int stack) { return stack <= 16 ? VR_STAGE_SLOTS : 0; }
+#endif
 constexpr int path_blocks_per_cu(int stack, int bt) { return 4 * path_waves(stack) * 64 / bt; }
 // LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
 // the node cache takes what the stacks leave (56 B per node)
 constexpr int path_cache_nodes(int stack, int bt) {
-    return (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)) / 56 > 0
-               ? (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)) / 56 : 1;
+    return (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)
+            - stage_slots(stack) * bt * 16) / 56 > 0
+               ? (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)
+                  - stage_slots(stack) * bt * 16) / 56 : 1;
 }
 
 #ifndef VR_XCD_BANDS
@@ -1528,7 +1547,9 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
     __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * BT : 1];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
-    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, (int)threadIdx.x);
+    __shared__ vr4 lds_stage[stage_slots(STACK) ? stage_slots(STACK) * BT : 1];
+    Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, (int)threadIdx.x);
+    L.stage = lds_stage;
     wave_body<STACK, FEAT, BT>(p, L);
 }
 
@@ -1546,6 +1567,7 @@ __global__ void __launch_bounds__(kLdsTreeBlock, 4) render_wave_kernel_lt(const 
     for (uint32_t i = (uint32_t)tid; i < 2u * p.n_nodes; i += (uint32_t)kLdsTreeBlock) lds_tree[i] = p.bvh16[i];
     __syncthreads();
     Lds L;
+    L.stage = nullptr;
     L.stk = nullptr;
     L.stk16 = lds_stk16 + tid;
     L.tstk = nullptr;
@@ -1615,17 +1637,31 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
     uint32_t wpaths = 0;
 #endif
+    // result staging (wave-uniform): the chunk each slot holds and the
+    // results it has received; st_sub = ~0u: free
+    constexpr int NS = ((FEAT & F_LDS_TREE) != 0u) ? 0 : stage_slots(STACK);
+    vr4* const stg = NS ? L.stage + (size_t)(tid >> 6) * (NS * 64) : nullptr;
+    uint32_t st_sub0 = ~0u, st_q0 = 0, st_n0 = 0, st_sub1 = ~0u, st_q1 = 0, st_n1 = 0;
+    auto alloc = [&](uint32_t sub, uint32_t path) -> int {     // a free staging slot for a new chunk, or -1
+        if (NS == 0 || sub == ~0u) return -1;
+        if (st_sub0 == ~0u) { st_sub0 = sub; st_q0 = path; st_n0 = 0; return 0; }
+        if (NS > 1 && st_sub1 == ~0u) { st_sub1 = sub; st_q1 = path; st_n1 = 0; return 1; }
+        return -1;                                         // both busy: this chunk stores directly
+    };
     uint32_t cur_sub, cur_q;
     grab(cur_sub, cur_q);                                  // wave-uniform: chunk being handed out
+    int cur_slot = alloc(cur_sub, cur_q);
     uint32_t next = 64u;                                   // items of the current chunk handed out
     int state = LS_DONE;
     uint32_t q = 0, slot = 0;                              // this lane's path and pixel slot
+    int my_slot = -1;                                      // staging slot of this lane's chunk
     Ray ray;
     PathState ps;
     HitRec hr;
     Trav tr;
-    auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
+    auto start = [&](uint32_t sub, uint32_t path, uint32_t px, int sslot) {   // render's per-sample prologue (:817-844)
         if (sub == ~0u) { state = LS_DONE; return; }
+        my_slot = sslot;
 #ifdef VR_PIXEL_MAJOR
         // the sub-tile's items pixel-major: a chunk holds all paths of
         // 64 / n_paths pixels, so a wave's bounce rays share their origins
@@ -1663,7 +1699,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         }
         state = LS_SHADE;
     };
-    start(cur_sub, cur_q, (uint32_t)lane);
+    start(cur_sub, cur_q, (uint32_t)lane, cur_slot);
 
     VR_T0(t_kernel);
     for (;;) {
@@ -1715,7 +1751,8 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 __builtin_nontemporal_store(vr_f32x4{ out.x, out.y, out.z, out.w },
                                             reinterpret_cast<vr_f32x4*>(p.paths + (size_t)q * p.path_stride + slot));
 #else
-                p.paths[(size_t)q * p.path_stride + slot] = out;
+                if (NS && my_slot >= 0) stg[my_slot * 64 + (int)(slot & 63u)] = out;   // staged (LDS)
+                else p.paths[(size_t)q * p.path_stride + slot] = out;
 #endif
                 ended = true;
             } else {
@@ -1729,15 +1766,31 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #ifdef VR_WAVE_TIMES
             wpaths += need;
 #endif
+            if (NS) {
+                // a staged chunk whose 64 results are all in: one coalesced 1-KB row store
+                st_n0 += (uint32_t)__popcll(__ballot(ended && my_slot == 0));
+                if (NS > 1) st_n1 += (uint32_t)__popcll(__ballot(ended && my_slot == 1));
+                if (st_n0 == 64u) {
+                    const vr4 v = stg[lane];
+                    p.paths[(size_t)st_q0 * p.path_stride + st_sub0 * 64u + (uint32_t)lane] = v;
+                    st_sub0 = ~0u; st_n0 = 0;
+                }
+                if (NS > 1 && st_n1 == 64u) {
+                    const vr4 v = stg[64 + lane];
+                    p.paths[(size_t)st_q1 * p.path_stride + st_sub1 * 64u + (uint32_t)lane] = v;
+                    st_sub1 = ~0u; st_n1 = 0;
+                }
+            }
             uint32_t nsub = cur_sub, nq = cur_q;
-            if (next + need > 64u && cur_sub != ~0u) grab(nsub, nq);
+            int nslot = cur_slot;
+            if (next + need > 64u && cur_sub != ~0u) { grab(nsub, nq); nslot = alloc(nsub, nq); }
             if (ended) {
                 const uint32_t r = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-                if (r < 64u) start(cur_sub, cur_q, r);
-                else start(nsub, nq, r - 64u);
+                if (r < 64u) start(cur_sub, cur_q, r, cur_slot);
+                else start(nsub, nq, r - 64u, nslot);
             }
-            if (next + need > 64u) { cur_sub = nsub; cur_q = nq; next = next + need - 64u; }
+            if (next + need > 64u) { cur_sub = nsub; cur_q = nq; cur_slot = nslot; next = next + need - 64u; }
             else next += need;
         }
         if (__ballot(state != LS_DONE) == 0ull) break;
