@@ -319,18 +319,25 @@ def test_path_split_is_result_invariant(native, cfg, frames):
         assert_bitexact(got[2], base[2], sc, f"depth split={split}")
 
 
-def test_multi_frame_launch_equals_frame_by_frame(native):
-    sc = scenes.make_scene("C1", 64, 64)
-    times = [5, 6, 7, 8]
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C5"])
+@pytest.mark.parametrize("sync", [True, False])
+def test_multi_frame_launch_equals_frame_by_frame(native, cfg, sync):
+    """One frame per call -- mesh scenes then trace the camera ray inside the
+    path kernel (no primary pass), synchronous calls run on the context stream
+    and unsynchronised ones overlap on the path streams -- accumulates exactly
+    what one multi-frame launch (shared primary records) does."""
+    sc = scenes.make_scene(cfg, 64, 64) if cfg != "C5" else scenes.make_scene(cfg, 96, 64)
+    times = [sc["time"] + i for i in range(4)] if cfg != "C1" else [5, 6, 7, 8]
     a4, r4, d4, _ = gpu_render(sc, 4, times)
     r = VRendererHIP(0)
     scenes.load_into(r, sc)
     for t in times:
-        r.render(frames=1, times=[t])
-    a1 = r.read_accum()
+        r.render(frames=1, times=[t], sync=sync)
+    a1, rgba1, d1 = r.read_accum(), r.read_rgba8(), r.read_depth8()
     assert r.getFrameCount() == 4
     r.cleanUp()
     assert np.array_equal(a4.view(np.uint32), a1.view(np.uint32))
+    assert np.array_equal(r4, rgba1) and np.array_equal(d4, d1)
 
 
 def test_pipelined_steps_bitexact_vs_portable_oracle(native, oracle):

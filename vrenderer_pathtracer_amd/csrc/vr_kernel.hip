@@ -1467,7 +1467,10 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
 //
 // Primary hits: the camera ray is the same for every path of a pixel (no
 // jitter, PathTracer.cu:842-844), so primary_kernel traces it once per pixel
-// per launch and every path of the pixel starts at its shading.
+// per launch and every path of the pixel starts at its shading.  Launches of
+// one frame (2 paths per pixel, the reference's render() cadence) skip that
+// serial pass (RenderParams::inline_prim): each path traces its camera ray in
+// the pool, where the primary pass's latency tail overlaps other lanes' work.
 //
 // Every path runs exactly the operations of trace(); only the interleaving
 // of paths on the SIMD changes, so results are bit-identical.
@@ -1685,6 +1688,11 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         uint32_t s2 = y * p.times[f];
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
         path_begin(ps, s1, s2);
+        if (p.inline_prim) {                               // few paths per pixel: trace the camera ray here
+            ray = camera_ray(p, x, y);
+            state = LS_SETUP;
+            return;
+        }
         if (CNT) cnt.ld128 += 2;
         const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
         hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
@@ -1889,7 +1897,7 @@ constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;      
 template <int STACK, uint32_t FEAT>
 static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
-    hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    if (!p.inline_prim) hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
     // one resident set: path_waves(STACK) waves per SIMD, 4 SIMDs per CU
     constexpr int BT = wave_block(STACK), BTS = wave_block_small(STACK);
     if (BTS != BT && p.small_blocks) {
@@ -1907,7 +1915,8 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 template <uint32_t FEAT>
 static void launch_wave_lt(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
-    hipLaunchKernelGGL((primary_kernel<kLdsTreeStack, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    if (!p.inline_prim)
+        hipLaunchKernelGGL((primary_kernel<kLdsTreeStack, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
     const size_t dyn = (size_t)p.n_nodes * 32u;
     static bool attr_set = false;                       // > 64 KB of dynamic LDS: raise the limit once
     if (!attr_set) {

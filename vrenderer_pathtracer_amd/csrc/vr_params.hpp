@@ -85,6 +85,7 @@ struct RenderParams {
     uint32_t wave_blocks;            // render_wave_kernel: CUs to fill with one resident set of blocks
     uint32_t small_blocks;           // render_wave_kernel: 256-thread blocks (launches of < 2^24 paths)
     uint32_t n_queues;               // render_wave_kernel: work queue heads in use (VR_QUEUES / VR_QUEUES_LARGE)
+    uint32_t inline_prim;            // render_wave_kernel: paths trace their own camera ray (no primary_kernel pass)
     const vr4* bvh;
     const vr4* bvh4;                 // 4-wide nodes, 7 rows each (culled traversal, VR_BVH4)
     uint32_t n_nodes4;

@@ -48,6 +48,11 @@ void dfree(T*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } }
 
 } // namespace
 
+// Launches of at most this many paths per pixel trace the camera ray in the
+// path kernel instead of a separate primary pass (RenderParams::inline_prim).
+#ifndef VR_INLINE_PRIM_PATHS
+#define VR_INLINE_PRIM_PATHS 2
+#endif
 // Path streams (see render_impl): launch i's kernels wait for the finish
 // pass of launch i - VR_PATH_STREAMS, the last reader of the same scratch.
 #ifndef VR_PATH_STREAMS
@@ -1089,11 +1094,6 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     }
     (void)hipGetLastError();            // launches below report their own errors only
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    if (p.use_scratch && c->join) {     // scene, stream or buffers changed: wait for all of `stream`
-        HIP_TRY(hipEventRecord(c->ev_join, c->stream));
-        for (auto& l : c->lane) HIP_TRY(hipStreamWaitEvent(l.s, c->ev_join, 0));
-        c->join = false;
-    }
     uint32_t done = 0;
     while (done < n_frames) {
         const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
@@ -1111,17 +1111,30 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // Without overlap every launch uses the same path stream, so it waits
         // for the previous one (and its finish pass, below) like a single stream.
         const bool small = (size_t)p.path_stride * 2u * k < ((size_t)1 << 24);
-        const bool ovl = c->overlap > 0 || (c->overlap < 0 && small);
+        // automatic overlap only behind a launch still in flight: a launch
+        // submitted to an idle device (one frame per synchronous call) runs
+        // its render and finish kernels on `stream` with no cross-stream waits
+        const bool ovl = c->overlap > 0 ||
+                         (c->overlap < 0 && small && c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
         p.small_blocks = small ? 1u : 0u;
+        p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
         p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? VR_QUEUES : VR_QUEUES_LARGE;
         if (!ovl) c->parity = 0;
         auto& l = c->lane[c->parity];
-        hipStream_t rs = p.use_scratch ? l.s : c->stream;
+        // overlapped launches run on the lane's path stream, the others on
+        // `stream` (in order behind everything queued there)
+        const bool on_lane = p.use_scratch && ovl;
+        hipStream_t rs = on_lane ? l.s : c->stream;
+        if (on_lane && c->join) {           // scene, stream or buffers changed: wait for all of `stream`
+            HIP_TRY(hipEventRecord(c->ev_join, c->stream));
+            for (auto& ln : c->lane) HIP_TRY(hipStreamWaitEvent(ln.s, c->ev_join, 0));
+            c->join = false;
+        }
         if (p.use_scratch) {
             if ((rc = ensure_lane(c, l, need, p.path_stride)) != VRHIP_OK) return rc;
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = l.paths; p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
-            if (l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
+            if (on_lane && l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
         }
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (n_tiles) {
@@ -1132,7 +1145,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         int e = vr::launch_render(p, n_tiles, stack, count, rs);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
         if (n_tiles) HIP_TRY(hipEventRecord(k1, rs));
-        if (p.use_scratch) {
+        if (on_lane) {
             HIP_TRY(hipEventRecord(l.done, rs));
             HIP_TRY(hipStreamWaitEvent(c->stream, l.done, 0));
         }
