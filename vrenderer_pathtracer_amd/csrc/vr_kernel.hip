@@ -1658,6 +1658,10 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     int state = LS_DONE;
     uint32_t q = 0, slot = 0;                              // this lane's path and pixel slot
     int my_slot = -1;                                      // staging slot of this lane's chunk
+#ifdef VR_PATH_TIMES
+    uint64_t pstart = 0;                                   // diagnostic: this lane's path start, primary hit kind
+    uint32_t pkind = 0;
+#endif
     Ray ray;
     PathState ps;
     HitRec hr;
@@ -1688,6 +1692,10 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         uint32_t s2 = y * p.times[f];
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
         path_begin(ps, s1, s2);
+#ifdef VR_PATH_TIMES
+        pstart = __builtin_amdgcn_s_memrealtime();
+        pkind = 15u;
+#endif
         if (p.inline_prim) {                               // few paths per pixel: trace the camera ray here
             ray = camera_ray(p, x, y);
             state = LS_SETUP;
@@ -1697,6 +1705,9 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
         hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
         hr.bv = b.x;
+#ifdef VR_PATH_TIMES
+        pkind = (uint32_t)hr.kind;
+#endif
         if constexpr (prim_has_dir<FEAT>()) {
             hr.su = hr.sv = 0.f;
             ray.o = p.cam_o;
@@ -1761,6 +1772,14 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #else
                 if (NS && my_slot >= 0) stg[my_slot * 64 + (int)(slot & 63u)] = out;   // staged (LDS)
                 else p.paths[(size_t)q * p.path_stride + slot] = out;
+#endif
+#ifdef VR_PATH_TIMES
+                const size_t pidx = (size_t)q * p.path_stride + slot;
+                if (p.counters && pidx < kPathTimesCap) {   // diagnostic: start, end | primary hit kind << 56 per path
+                    unsigned long long* pr = p.counters + kWaveTimesBase + 3 * 8192 + 2 * pidx;
+                    pr[0] = pstart;
+                    pr[1] = __builtin_amdgcn_s_memrealtime() | ((unsigned long long)pkind << 56);
+                }
 #endif
                 ended = true;
             } else {

@@ -50,6 +50,7 @@ constexpr int kCounters = 8;
 constexpr int kExecCounterBase = 16;
 constexpr int kExecCounters = 8;
 constexpr int kWaveTimesBase = 32;   // -DVR_WAVE_TIMES diagnostic builds: per-wave records from here
+constexpr size_t kPathTimesCap = 4u * 1024u * 1024u;   // -DVR_PATH_TIMES: per-path records after them (paths of a launch)
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
 // render_wave_kernel work queues: RenderParams::n_queues counters (a power of

@@ -915,7 +915,9 @@ int vrhip_gl_present(vrhip_ctx* c)
     return VRHIP_OK;
 }
 
-#ifdef VR_WAVE_TIMES
+#if defined(VR_WAVE_TIMES) && defined(VR_PATH_TIMES)
+constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192 + 2 * (int)vr::kPathTimesCap;   // + 2 per path
+#elif defined(VR_WAVE_TIMES)
 constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192;   // + per-wave start / end / paths of render_wave_kernel
 #else
 constexpr int kDebugSlots = vr::kWaveTimesBase;
@@ -1250,10 +1252,10 @@ int vrhip_debug_counters(vrhip_ctx* c, uint64_t out[16], int reset)
 // diagnostic build only (not in vrhip.h): per-wave start, end, paths of the last wave-kernel launch
 extern "C" int vrhip_debug_wave_times(vrhip_ctx* c, uint64_t* out, uint32_t n_waves)
 {
-    if (!c || !out || n_waves > 8192) return fail(VRHIP_ERR_INVALID, "bad argument");
+    if (!c || !out || 3 * (size_t)n_waves > (size_t)(kDebugSlots - vr::kWaveTimesBase)) return fail(VRHIP_ERR_INVALID, "bad argument");
     int rc = set_device(c); if (rc) return rc;
     if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(out, c->counters + 16, sizeof(uint64_t) * 3 * n_waves, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->counters + vr::kWaveTimesBase, sizeof(uint64_t) * 3 * n_waves, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return VRHIP_OK;
 }
