@@ -46,7 +46,7 @@ int vrhip_device_count(int *count);
 /* ---- lifetime -------------------------------------------------------- */
 /* replaces vRendererCuda::init (src/vRendererCuda.cpp:38-55): allocates the
  * float4[W*H] accumulation buffer and the RGBA8 colour/depth images on
- * `device`, zero-fills, frame counter = 1. */
+ * `device`, zero-fills, frame counter = 1.  1 <= width, height <= 65535. */
 int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx **out);
 /* replaces vRendererCuda::cleanUp + cu_cleanUp (src/vRendererCuda.cpp:167-199,
  * cuda/src/PathTracer.cu:1009-1030). NULL is a no-op. */

@@ -265,7 +265,6 @@ constexpr bool kFp16Nodes = false;
 #endif
 
 struct Lds {
-    vr4* stage;               // path kernel: this block's path-result staging rows (stage_slots)
     int* stk;                 // this thread's column of the stack
     unsigned short* stk16;    // F_LDS_TREE: 16-bit entries, (parent node << 1) | child slot; 0xffff = sentinel
     unsigned short* tstk;     // entry distance of each stacked child (bf16, rounded down)
@@ -1244,6 +1243,25 @@ __device__ __forceinline__ u8x4 tonemap(vr4 io, uint32_t frame) {
     return c;
 }
 
+// A path's result in the scratch (RenderParams::paths).  Its .w is the
+// primary hit's depth term (bounce_step: set at bounce 0 and returned on
+// every exit) except for a Cornell-box escape, which returns 0 -- so outside
+// Cornell scenes all paths of a pixel carry the same .w, stored once (by
+// path 0) in path_w, and rows hold 12-B radiances: a quarter less scratch
+// written by the path kernel and read by finish_kernel (HBM-bound).
+__device__ __forceinline__ bool paths_rgba(const RenderParams& p) { return (p.flags & F_CORNELL) != 0u; }
+template <uint32_t FEAT>
+__device__ __forceinline__ void store_path(const RenderParams& p, uint32_t q, uint32_t slot, const vr4& out)
+{
+    const size_t i = (size_t)q * p.path_stride + slot;
+    if (HAS(F_CORNELL)) {
+        static_cast<vr4*>(p.paths)[i] = out;
+    } else {
+        static_cast<vr3*>(p.paths)[i] = vr3{ out.x, out.y, out.z };
+        if (q == 0u) p.path_w[slot] = out.w;
+    }
+}
+
 // Split launches: sums each pixel's path results in path order (the same
 // float4 operations, in the same order, as the unsplit kernel), then writes
 // the accumulation, colour and depth.
@@ -1262,13 +1280,24 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     const uint32_t ind = x + y * p.W;
     vr4 io = p.first_frame != 1u ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
     const uint32_t n_paths = 2u * p.n_frames;
-    const vr4* src = p.paths + (size_t)tile * kBlockThreads + tid;
-    vr4 result = mk4(0.f, 0.f, 0.f, 0.f);
-    for (uint32_t q = 0; q < n_paths; ++q) {
-        result = src[(size_t)q * p.path_stride];
-        io = add4(io, mul4s(result, 1.f / 2.f));
+    const uint32_t slot = tile * kBlockThreads + tid;
+    float last_w = 0.f;
+    if (paths_rgba(p)) {
+        const vr4* src = static_cast<const vr4*>(p.paths) + slot;
+        for (uint32_t q = 0; q < n_paths; ++q) {
+            const vr4 r = src[(size_t)q * p.path_stride];
+            io = add4(io, mul4s(r, 1.f / 2.f));
+            last_w = r.w;
+        }
+    } else {
+        const vr3* src = static_cast<const vr3*>(p.paths) + slot;
+        last_w = p.path_w[slot];
+        for (uint32_t q = 0; q < n_paths; ++q) {
+            const vr3 r = src[(size_t)q * p.path_stride];
+            io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
+        }
     }
-    const unsigned char db = f2u8((1.f - result.w) * 255);
+    const unsigned char db = f2u8((1.f - last_w) * 255);
     u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
     p.depth[ind] = dv;
     p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
@@ -1310,8 +1339,10 @@ __device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, 
 // Camera ray through pixel (x, y) (PathTracer.cu:842-844: no jitter).
 __device__ __forceinline__ Ray camera_ray(const RenderParams& p, uint32_t x, uint32_t y)
 {
-    const float sx = (float)((0.25 + (double)x) / (double)p.W - 0.5);
-    const float sy = (float)((0.25 + (double)y) / (double)p.H - 0.5);
+    // (float)((0.25 + x) / W - 0.5) and the same for y, evaluated in double
+    // on the host once per column / row (vrhip_create)
+    const float sx = p.cam_sxy[x];
+    const float sy = p.cam_sxy[p.W + y];
     Ray cam;
     cam.o = p.cam_o;
     cam.d = normalize4(add4(add4(p.cam_d, mul4s(p.cx, sx)), mul4s(p.cy, sy)));
@@ -1378,7 +1409,7 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
         if (direct)
             io = add4(io, mul4s(result, 1.f / 2.f));
         else
-            p.paths[(size_t)q * p.path_stride + (size_t)tile * kBlockThreads + tid] = result;
+            store_path<FEAT>(p, q, tile * kBlockThreads + (uint32_t)tid, result);
         last_w = result.w;
     }
     if (direct) {   // else finish_kernel accumulates the paths' results in path order
@@ -1481,7 +1512,7 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
 #ifndef VR_SHADE_RATIO
 #define VR_SHADE_RATIO 1
 #endif
-enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3 };
+enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3, LS_CAMERA = 4 };
 
 // Block size of the path kernel: its blocks hold no tiles, so one block of
 // 1,024 threads per CU shares one LDS node cache four times the size of a
@@ -1509,30 +1540,12 @@ constexpr int wave_block(int stack) { return stack <= kQ4Stack ? VR_PATH_BLOCK :
 // 0.420 ms), while whole frames keep the 768-thread blocks (C2 3,437 vs 3,244).
 constexpr int wave_block_small(int stack) { return stack <= kQ4Stack ? kBlockThreads : wave_block(stack); }
 constexpr int path_waves(int stack) { return stack <= kQ4Stack ? VR_PATH_WAVES : stack <= 32 ? 4 : 2; }
-// Path-result staging (opt-in, -DVR_STAGE_SLOTS=n): per wave, n rows of 64
-// results (1 KB each) in LDS, one per chunk in flight; a chunk's row is
-// written to the scratch with one coalesced store when its 64 paths have
-// ended, instead of scattered 16-B stores that leave lines partially written
-// in L2 (WRITE_SIZE 1.8x the result bytes on C2).  Measured: 2 slots C2 -3 %,
-// C3 -8 %, WRITE_SIZE 2.6x (the slot bookkeeping spills to scratch, and a
-// chunk finds no free slot while stragglers of older chunks hold both);
-// 3 slots 97 VGPRs, C2 -35 %, 1.6x.  Stack classes with room in LDS only.
-#ifndef VR_STAGE_SLOTS
-#define VR_STAGE_SLOTS 0
-#endif
-#ifdef VR_PIXEL_MAJOR
-constexpr int stage_slots(int stack) { return 0 * stack; }   // chunks are not contiguous result rows
-#else
-constexpr int stage_slots(int stack) { return stack <= 16 ? VR_STAGE_SLOTS : 0; }
-#endif
 constexpr int path_blocks_per_cu(int stack, int bt) { return 4 * path_waves(stack) * 64 / bt; }
 // LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
 // the node cache takes what the stacks leave (56 B per node)
 constexpr int path_cache_nodes(int stack, int bt) {
-    return (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)
-            - stage_slots(stack) * bt * 16) / 56 > 0
-               ? (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)
-                  - stage_slots(stack) * bt * 16) / 56 : 1;
+    return (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)) / 56 > 0
+               ? (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)) / 56 : 1;
 }
 
 #ifndef VR_XCD_BANDS
@@ -1542,6 +1555,18 @@ constexpr int path_cache_nodes(int stack, int bt) {
 template <int STACK, uint32_t FEAT, int BT>
 __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L);
 
+// Pixel of item `px` of this rank's 8x8 sub-tile `sub` (wave-uniform in the
+// path kernel, so the tile arithmetic, a division included, stays scalar).
+__device__ __forceinline__ void sub_pixel(const RenderParams& p, uint32_t sub, uint32_t px, uint32_t& x, uint32_t& y)
+{
+    const uint32_t tile = sub >> 2, quad = sub & 3u;
+    const uint32_t gtile = p.rank + tile * p.nranks;       // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    x = tile_x * 16u + (quad & 1u) * 8u + (px & 7u);
+    y = tile_y * 16u + (quad >> 1) * 8u + (px >> 3);
+}
+
 template <int STACK, uint32_t FEAT, int BT>
 __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(const RenderParams p)
 {
@@ -1550,9 +1575,7 @@ __global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(cons
     __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * BT : 1];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
-    __shared__ vr4 lds_stage[stage_slots(STACK) ? stage_slots(STACK) * BT : 1];
-    Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, (int)threadIdx.x);
-    L.stage = lds_stage;
+    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, (int)threadIdx.x);
     wave_body<STACK, FEAT, BT>(p, L);
 }
 
@@ -1570,7 +1593,6 @@ __global__ void __launch_bounds__(kLdsTreeBlock, 4) render_wave_kernel_lt(const 
     for (uint32_t i = (uint32_t)tid; i < 2u * p.n_nodes; i += (uint32_t)kLdsTreeBlock) lds_tree[i] = p.bvh16[i];
     __syncthreads();
     Lds L;
-    L.stage = nullptr;
     L.stk = nullptr;
     L.stk16 = lds_stk16 + tid;
     L.tstk = nullptr;
@@ -1640,24 +1662,12 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
     uint32_t wpaths = 0;
 #endif
-    // result staging (wave-uniform): the chunk each slot holds and the
-    // results it has received; st_sub = ~0u: free
-    constexpr int NS = ((FEAT & F_LDS_TREE) != 0u) ? 0 : stage_slots(STACK);
-    vr4* const stg = NS ? L.stage + (size_t)(tid >> 6) * (NS * 64) : nullptr;
-    uint32_t st_sub0 = ~0u, st_q0 = 0, st_n0 = 0, st_sub1 = ~0u, st_q1 = 0, st_n1 = 0;
-    auto alloc = [&](uint32_t sub, uint32_t path) -> int {     // a free staging slot for a new chunk, or -1
-        if (NS == 0 || sub == ~0u) return -1;
-        if (st_sub0 == ~0u) { st_sub0 = sub; st_q0 = path; st_n0 = 0; return 0; }
-        if (NS > 1 && st_sub1 == ~0u) { st_sub1 = sub; st_q1 = path; st_n1 = 0; return 1; }
-        return -1;                                         // both busy: this chunk stores directly
-    };
     uint32_t cur_sub, cur_q;
     grab(cur_sub, cur_q);                                  // wave-uniform: chunk being handed out
-    int cur_slot = alloc(cur_sub, cur_q);
     uint32_t next = 64u;                                   // items of the current chunk handed out
     int state = LS_DONE;
     uint32_t q = 0, slot = 0;                              // this lane's path and pixel slot
-    int my_slot = -1;                                      // staging slot of this lane's chunk
+    uint32_t cam_xy = 0;                                   // F_INLINE_PRIM: its pixel (x << 16 | y) until LS_CAMERA
 #ifdef VR_PATH_TIMES
     uint64_t pstart = 0;                                   // diagnostic: this lane's path start, primary hit kind
     uint32_t pkind = 0;
@@ -1666,9 +1676,8 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     PathState ps;
     HitRec hr;
     Trav tr;
-    auto start = [&](uint32_t sub, uint32_t path, uint32_t px, int sslot) {   // render's per-sample prologue (:817-844)
+    auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
         if (sub == ~0u) { state = LS_DONE; return; }
-        my_slot = sslot;
 #ifdef VR_PIXEL_MAJOR
         // the sub-tile's items pixel-major: a chunk holds all paths of
         // 64 / n_paths pixels, so a wave's bounce rays share their origins
@@ -1682,12 +1691,8 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #endif
         slot = sub * 64u + px;
         const uint32_t f = q >> 1;
-        const uint32_t tile = sub >> 2, quad = sub & 3u;
-        const uint32_t gtile = p.rank + tile * p.nranks;   // tiles dealt round-robin to ranks
-        const uint32_t tile_y = gtile / p.tiles_x;
-        const uint32_t tile_x = gtile - tile_y * p.tiles_x;
-        const uint32_t x = tile_x * 16u + (quad & 1u) * 8u + (px & 7u);
-        const uint32_t y = tile_y * 16u + (quad >> 1) * 8u + (px >> 3);
+        uint32_t x, y;
+        sub_pixel(p, sub, px, x, y);
         uint32_t s1 = x * (p.first_frame + f);
         uint32_t s2 = y * p.times[f];
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
@@ -1696,9 +1701,9 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         pstart = __builtin_amdgcn_s_memrealtime();
         pkind = 15u;
 #endif
-        if (p.inline_prim) {                               // few paths per pixel: trace the camera ray here
-            ray = camera_ray(p, x, y);
-            state = LS_SETUP;
+        if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {      // few paths per pixel: trace the camera ray here
+            cam_xy = (x << 16) | y;                        // (set up at the top of the loop, out of the refill)
+            state = LS_CAMERA;
             return;
         }
         if (CNT) cnt.ld128 += 2;
@@ -1718,11 +1723,17 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         }
         state = LS_SHADE;
     };
-    start(cur_sub, cur_q, (uint32_t)lane, cur_slot);
+    start(cur_sub, cur_q, (uint32_t)lane);
 
     VR_T0(t_kernel);
     for (;;) {
         VR_T0(t_setup);
+        if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {
+            if (state == LS_CAMERA) {
+                ray = camera_ray(p, cam_xy >> 16, cam_xy & 0xffffu);
+                state = LS_SETUP;
+            }
+        }
         if (state == LS_SETUP) {
             if (intersect_spheres<CNT, FEAT>(p, ray, hr, cnt)) {
                 trav_init<FEAT, stack_cull(STACK)>(p, ray, hr.t, tr, L);
@@ -1765,14 +1776,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             VR_LANE(4, 5);
             vr4 out;
             if (bounce_step<CNT, FEAT>(p, ray, hr, ps, out, cnt)) {
-#ifdef VR_PATH_STORE_NT
-                typedef float vr_f32x4 __attribute__((ext_vector_type(4)));
-                __builtin_nontemporal_store(vr_f32x4{ out.x, out.y, out.z, out.w },
-                                            reinterpret_cast<vr_f32x4*>(p.paths + (size_t)q * p.path_stride + slot));
-#else
-                if (NS && my_slot >= 0) stg[my_slot * 64 + (int)(slot & 63u)] = out;   // staged (LDS)
-                else p.paths[(size_t)q * p.path_stride + slot] = out;
-#endif
+                store_path<FEAT>(p, q, slot, out);
 #ifdef VR_PATH_TIMES
                 const size_t pidx = (size_t)q * p.path_stride + slot;
                 if (p.counters && pidx < kPathTimesCap) {   // diagnostic: start, end | primary hit kind << 56 per path
@@ -1793,31 +1797,15 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #ifdef VR_WAVE_TIMES
             wpaths += need;
 #endif
-            if (NS) {
-                // a staged chunk whose 64 results are all in: one coalesced 1-KB row store
-                st_n0 += (uint32_t)__popcll(__ballot(ended && my_slot == 0));
-                if (NS > 1) st_n1 += (uint32_t)__popcll(__ballot(ended && my_slot == 1));
-                if (st_n0 == 64u) {
-                    const vr4 v = stg[lane];
-                    p.paths[(size_t)st_q0 * p.path_stride + st_sub0 * 64u + (uint32_t)lane] = v;
-                    st_sub0 = ~0u; st_n0 = 0;
-                }
-                if (NS > 1 && st_n1 == 64u) {
-                    const vr4 v = stg[64 + lane];
-                    p.paths[(size_t)st_q1 * p.path_stride + st_sub1 * 64u + (uint32_t)lane] = v;
-                    st_sub1 = ~0u; st_n1 = 0;
-                }
-            }
             uint32_t nsub = cur_sub, nq = cur_q;
-            int nslot = cur_slot;
-            if (next + need > 64u && cur_sub != ~0u) { grab(nsub, nq); nslot = alloc(nsub, nq); }
+            if (next + need > 64u && cur_sub != ~0u) grab(nsub, nq);
             if (ended) {
                 const uint32_t r = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-                if (r < 64u) start(cur_sub, cur_q, r, cur_slot);
-                else start(nsub, nq, r - 64u, nslot);
+                if (r < 64u) start(cur_sub, cur_q, r);
+                else start(nsub, nq, r - 64u);
             }
-            if (next + need > 64u) { cur_sub = nsub; cur_q = nq; cur_slot = nslot; next = next + need - 64u; }
+            if (next + need > 64u) { cur_sub = nsub; cur_q = nq; next = next + need - 64u; }
             else next += need;
         }
         if (__ballot(state != LS_DONE) == 0ull) break;
@@ -1916,7 +1904,10 @@ constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;      
 template <int STACK, uint32_t FEAT>
 static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
-    if (!p.inline_prim) hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    if constexpr ((FEAT & F_INLINE_PRIM) == 0u) {
+        if (p.inline_prim) { launch_wave<STACK, FEAT | F_INLINE_PRIM>(p, n_tiles, s); return; }
+        hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    }
     // one resident set: path_waves(STACK) waves per SIMD, 4 SIMDs per CU
     constexpr int BT = wave_block(STACK), BTS = wave_block_small(STACK);
     if (BTS != BT && p.small_blocks) {
@@ -1934,8 +1925,10 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 template <uint32_t FEAT>
 static void launch_wave_lt(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
-    if (!p.inline_prim)
+    if constexpr ((FEAT & F_INLINE_PRIM) == 0u) {
+        if (p.inline_prim) { launch_wave_lt<FEAT | F_INLINE_PRIM>(p, n_tiles, s); return; }
         hipLaunchKernelGGL((primary_kernel<kLdsTreeStack, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    }
     const size_t dyn = (size_t)p.n_nodes * 32u;
     static bool attr_set = false;                       // > 64 KB of dynamic LDS: raise the limit once
     if (!attr_set) {

@@ -30,6 +30,10 @@ enum Flags : uint32_t {
     F_COUNT_EXEC = 1u << 10,
     F_Q4 = 1u << 11,         // culled traversal over the quantized 4-wide nodes (bvhq)
     F_LDS_TREE = 1u << 12,   // culled traversal with the whole fp16 tree in each block's LDS
+    // compile-time only: the path kernel of launches with RenderParams::inline_prim
+    // (paths trace their own camera ray; a separate instantiation, so the
+    // multi-frame kernels keep the registers that code would take)
+    F_INLINE_PRIM = 1u << 13,
 };
 // LDS-resident tree walk: one 1024-thread block per CU (4 waves/SIMD), the
 // fp16 tree (32 B per node) in dynamic LDS next to 16-bit stacks of kLdsTreeStack entries
@@ -39,6 +43,7 @@ constexpr int kLdsBytesPerCU = 163840;
 constexpr int kQ4Stack = 26;         // stack class of the quantized 4-wide walk: 3 pushes per level, depth <= 8
 
 constexpr int kMaxFramesPerLaunch = 64;
+
 // counting variants, slots [0, kCounters): rays, node visits, vert0 slot
 // reads, triangle tests, attribute bytes, texture fetches, HDRI fetches, BRDF
 // lookups.  The instrumented production kernels also fill slots
@@ -72,6 +77,7 @@ constexpr uint32_t kQueueStride = 256;
 struct RenderParams {
     vr4 cam_o, cam_d, cx, cy;        // cx, cy precomputed exactly as PathTracer.cu:833-836
     uint32_t W, H, wr, hr;           // wr/hr: rendered region (grid truncation, :888-889)
+    const float* cam_sxy;            // camera-ray screen offsets per column [W] then per row [H] (:842-843)
     float fresnel_coef, fresnel_pow;
     uint32_t flags;
     uint32_t tiles_x;                // wr / 16
@@ -80,13 +86,18 @@ struct RenderParams {
     uint32_t split;                  // path groups per pixel (blocks per tile)
     uint32_t use_scratch;            // 1: paths store radiance to `paths`, finish_kernel accumulates
     uint32_t path_stride;            // owned tiles * 256 (scratch row length)
-    vr4* paths;                      // per-path results [2*n_frames][path_stride]
+    // per-path results [2*n_frames][path_stride]: float4 (radiance, .w) in
+    // Cornell scenes; elsewhere every path of a pixel has the same .w (the
+    // primary hit's depth), so rows hold the radiance (12 B) and path_w
+    // [path_stride] the .w once per pixel (vr_kernel.hip store_path)
+    void* paths;
+    float* path_w;
     vr4* prim;                       // per owned pixel: the camera ray's closest hit (2 x vr4, primary_kernel)
     uint32_t* chunk_ctr;             // render_wave_kernel's work queue heads (zeroed by finish_kernel)
     uint32_t wave_blocks;            // render_wave_kernel: CUs to fill with one resident set of blocks
     uint32_t small_blocks;           // render_wave_kernel: 256-thread blocks (launches of < 2^24 paths)
     uint32_t n_queues;               // render_wave_kernel: work queue heads in use (VR_QUEUES / VR_QUEUES_LARGE)
-    uint32_t inline_prim;            // render_wave_kernel: paths trace their own camera ray (no primary_kernel pass)
+    uint32_t inline_prim;            // paths trace their own camera ray (no primary_kernel pass; F_INLINE_PRIM kernel)
     const vr4* bvh;
     const vr4* bvh4;                 // 4-wide nodes, 7 rows each (culled traversal, VR_BVH4)
     uint32_t n_nodes4;

@@ -65,6 +65,7 @@ struct vrhip_ctx {
     hipStream_t stream = nullptr;
     uint32_t W = 0, H = 0;
     vr4* accum = nullptr;
+    float* cam_sxy = nullptr;                   // camera-ray screen offsets: W column values, then H row values
     vr::u8x4* rgba = nullptr;
     vr::u8x4* depth = nullptr;
     // camera (vCamera, cuda/include/PathTracer.cuh:58-84)
@@ -635,7 +636,8 @@ int vrhip_device_count(int* count)
 
 int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
 {
-    if (!out || width == 0 || height == 0) return fail(VRHIP_ERR_INVALID, "bad create arguments");
+    if (!out || width == 0 || height == 0 || width > 65535 || height > 65535)
+        return fail(VRHIP_ERR_INVALID, "bad create arguments (1..65535 pixels per side)");
     *out = nullptr;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(VRHIP_ERR_NO_DEVICE, "no HIP device");
@@ -668,6 +670,18 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
         return cleanup(fail(VRHIP_ERR_NOMEM, "hipMalloc of frame buffers failed"));
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
         return cleanup(fail(VRHIP_ERR_HIP, "hipEventCreate failed"));
+    {
+        // the camera ray's screen offsets (PathTracer.cu:842-843), evaluated
+        // in double as there, once per column and row: the kernels index
+        // them instead of dividing in f64 per ray
+        std::vector<float> sxy((size_t)width + height);
+        for (uint32_t x = 0; x < width; ++x) sxy[x] = (float)((0.25 + (double)x) / (double)width - 0.5);
+        for (uint32_t y = 0; y < height; ++y) sxy[(size_t)width + y] = (float)((0.25 + (double)y) / (double)height - 0.5);
+        if (hipMalloc((void**)&c->cam_sxy, sizeof(float) * sxy.size()) != hipSuccess)
+            return cleanup(fail(VRHIP_ERR_NOMEM, "hipMalloc of the camera table failed"));
+        if (hipMemcpy(c->cam_sxy, sxy.data(), sizeof(float) * sxy.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return cleanup(fail(VRHIP_ERR_HIP, "camera table upload failed"));
+    }
     if (hipMemsetAsync(c->rgba, 0, 4 * npx, c->stream) != hipSuccess ||
         hipMemsetAsync(c->depth, 0, 4 * npx, c->stream) != hipSuccess)
         return cleanup(fail(VRHIP_ERR_HIP, "hipMemset failed"));
@@ -683,7 +697,7 @@ int vrhip_destroy(vrhip_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     quiesce(c);
-    dfree(c->accum); dfree(c->rgba); dfree(c->depth);
+    dfree(c->accum); dfree(c->rgba); dfree(c->depth); dfree(c->cam_sxy);
     dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->bvhq); dfree(c->verts); dfree(c->tri_e); dfree(c->tpath); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     for (int i = 0; i < 2; ++i)
@@ -1030,6 +1044,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.cx = vr4{ sx * c->cam_right[0], sx * c->cam_right[1], sx * c->cam_right[2], 0.f };
     p.cy = vr4{ c->fov_scale * c->cam_up[0], c->fov_scale * c->cam_up[1], c->fov_scale * c->cam_up[2], 0.f };
     p.W = c->W; p.H = c->H;
+    p.cam_sxy = c->cam_sxy;
     p.wr = (c->W / 16u) * 16u; p.hr = rendered_rows(c);
     p.fresnel_coef = c->fresnel_coef; p.fresnel_pow = c->fresnel_pow;
     uint32_t f = 0;
@@ -1135,7 +1150,8 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         if (p.use_scratch) {
             if ((rc = ensure_lane(c, l, need, p.path_stride)) != VRHIP_OK) return rc;
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
-            p.paths = l.paths; p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
+            p.paths = l.paths; p.path_w = reinterpret_cast<float*>(reinterpret_cast<vr::vr3*>(l.paths) + need);
+            p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
             if (on_lane && l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
         }
         hipEvent_t k0 = nullptr, k1 = nullptr;
