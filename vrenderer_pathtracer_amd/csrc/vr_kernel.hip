@@ -1089,7 +1089,12 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
             out = ps.accum;
             return true;
         }
-        out = mk4(0.f, 0.f, 0.f, 0.f);
+        // Cornell escape (:649-650): radiance and .w are 0.  The x channel
+        // is -0.0 -- equal to +0 in every sum it enters (a running sum that
+        // starts at +0 under round-to-nearest is never -0, so adding -0 or +0
+        // leaves its bits unchanged) -- and marks the escape in the
+        // path-result scratch, which does not store .w (store_path).
+        out = mk4(-0.f, 0.f, 0.f, 0.f);
         return true;
     }
     if (!ref_alg<COUNT, FEAT>() && ps.bounce == 3) {
@@ -1211,7 +1216,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
 
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit0, uint32_t& s0, uint32_t& s1,
-                     const Lds& L, Cnt& cnt)
+                     const Lds& L, Cnt& cnt, float& depth)
 {
     PathState ps;
     path_begin(ps, s0, s1);
@@ -1226,7 +1231,7 @@ __device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit
             (void)intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, L, cnt);
         }
         vr4 out;
-        if (bounce_step<COUNT, FEAT>(p, ray, hr, ps, out, cnt)) return out;
+        if (bounce_step<COUNT, FEAT>(p, ray, hr, ps, out, cnt)) { depth = ps.depth; return out; }
     }
 }
 
@@ -1243,23 +1248,19 @@ __device__ __forceinline__ u8x4 tonemap(vr4 io, uint32_t frame) {
     return c;
 }
 
-// A path's result in the scratch (RenderParams::paths).  Its .w is the
-// primary hit's depth term (bounce_step: set at bounce 0 and returned on
-// every exit) except for a Cornell-box escape, which returns 0 -- so outside
-// Cornell scenes all paths of a pixel carry the same .w, stored once (by
-// path 0) in path_w, and rows hold 12-B radiances: a quarter less scratch
-// written by the path kernel and read by finish_kernel (HBM-bound).
-__device__ __forceinline__ bool paths_rgba(const RenderParams& p) { return (p.flags & F_CORNELL) != 0u; }
-template <uint32_t FEAT>
-__device__ __forceinline__ void store_path(const RenderParams& p, uint32_t q, uint32_t slot, const vr4& out)
+// A path's result in the scratch (RenderParams::paths): its radiance, 12 B.
+// The .w bounce_step returns is the primary hit's depth term (ps.depth, set
+// at bounce 0, the same for every path of a pixel: no camera jitter) on
+// every exit but a Cornell escape, which returns 0 and marks itself with
+// x = -0.0.  So .w is not stored per path: path 0 of the pixel stores the
+// depth term once (path_w) and finish_kernel rebuilds each path's .w from
+// it and the escape mark -- a quarter less scratch written by the path
+// kernel and read by the (HBM-bound) finish pass.
+__device__ __forceinline__ bool escaped(float x) { return __float_as_uint(x) == 0x80000000u; }
+__device__ __forceinline__ void store_path(const RenderParams& p, uint32_t q, uint32_t slot, const vr4& out, float depth)
 {
-    const size_t i = (size_t)q * p.path_stride + slot;
-    if (HAS(F_CORNELL)) {
-        static_cast<vr4*>(p.paths)[i] = out;
-    } else {
-        static_cast<vr3*>(p.paths)[i] = vr3{ out.x, out.y, out.z };
-        if (q == 0u) p.path_w[slot] = out.w;
-    }
+    p.paths[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
+    if (q == 0u) p.path_w[slot] = depth;
 }
 
 // Split launches: sums each pixel's path results in path order (the same
@@ -1281,21 +1282,14 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     vr4 io = p.first_frame != 1u ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
     const uint32_t n_paths = 2u * p.n_frames;
     const uint32_t slot = tile * kBlockThreads + tid;
+    const vr3* src = p.paths + slot;
+    const float depth = p.path_w[slot];
+    const bool cornell = (p.flags & F_CORNELL) != 0u;
     float last_w = 0.f;
-    if (paths_rgba(p)) {
-        const vr4* src = static_cast<const vr4*>(p.paths) + slot;
-        for (uint32_t q = 0; q < n_paths; ++q) {
-            const vr4 r = src[(size_t)q * p.path_stride];
-            io = add4(io, mul4s(r, 1.f / 2.f));
-            last_w = r.w;
-        }
-    } else {
-        const vr3* src = static_cast<const vr3*>(p.paths) + slot;
-        last_w = p.path_w[slot];
-        for (uint32_t q = 0; q < n_paths; ++q) {
-            const vr3 r = src[(size_t)q * p.path_stride];
-            io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
-        }
+    for (uint32_t q = 0; q < n_paths; ++q) {
+        const vr3 r = src[(size_t)q * p.path_stride];
+        last_w = (cornell && escaped(r.x)) ? 0.f : depth;
+        io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
     }
     const unsigned char db = f2u8((1.f - last_w) * 255);
     u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
@@ -1405,11 +1399,12 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
             s2 = y * p.times[f];
             if (q & 1u) (void)hash_seeds(s1, s2);
         }
-        const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, L, cnt);
+        float depth;
+        const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, L, cnt, depth);
         if (direct)
             io = add4(io, mul4s(result, 1.f / 2.f));
         else
-            store_path<FEAT>(p, q, tile * kBlockThreads + (uint32_t)tid, result);
+            store_path(p, q, tile * kBlockThreads + (uint32_t)tid, result, depth);
         last_w = result.w;
     }
     if (direct) {   // else finish_kernel accumulates the paths' results in path order
@@ -1776,7 +1771,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             VR_LANE(4, 5);
             vr4 out;
             if (bounce_step<CNT, FEAT>(p, ray, hr, ps, out, cnt)) {
-                store_path<FEAT>(p, q, slot, out);
+                store_path(p, q, slot, out, ps.depth);
 #ifdef VR_PATH_TIMES
                 const size_t pidx = (size_t)q * p.path_stride + slot;
                 if (p.counters && pidx < kPathTimesCap) {   // diagnostic: start, end | primary hit kind << 56 per path

@@ -86,11 +86,10 @@ struct RenderParams {
     uint32_t split;                  // path groups per pixel (blocks per tile)
     uint32_t use_scratch;            // 1: paths store radiance to `paths`, finish_kernel accumulates
     uint32_t path_stride;            // owned tiles * 256 (scratch row length)
-    // per-path results [2*n_frames][path_stride]: float4 (radiance, .w) in
-    // Cornell scenes; elsewhere every path of a pixel has the same .w (the
-    // primary hit's depth), so rows hold the radiance (12 B) and path_w
-    // [path_stride] the .w once per pixel (vr_kernel.hip store_path)
-    void* paths;
+    // per-path radiances [2*n_frames][path_stride] and, per slot, the
+    // pixel's depth term, from which finish_kernel rebuilds each path's .w
+    // (vr_kernel.hip store_path)
+    vr3* paths;
     float* path_w;
     vr4* prim;                       // per owned pixel: the camera ray's closest hit (2 x vr4, primary_kernel)
     uint32_t* chunk_ctr;             // render_wave_kernel's work queue heads (zeroed by finish_kernel)

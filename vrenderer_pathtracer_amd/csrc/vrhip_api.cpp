@@ -1150,7 +1150,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         if (p.use_scratch) {
             if ((rc = ensure_lane(c, l, need, p.path_stride)) != VRHIP_OK) return rc;
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
-            p.paths = l.paths; p.path_w = reinterpret_cast<float*>(reinterpret_cast<vr::vr3*>(l.paths) + need);
+            p.paths = reinterpret_cast<vr::vr3*>(l.paths); p.path_w = reinterpret_cast<float*>(p.paths + need);
             p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
             if (on_lane && l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
         }
