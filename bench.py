@@ -134,6 +134,19 @@ def hbm_traffic(cfg: str):
         return None, None
 
 
+def unit_busy(cfg: str):
+    """Busy fractions of the CU units the path kernel is bound by, from the
+    rocprofv3 counter passes of this config (profiles/units_<cfg>.json,
+    scripts/summarize_mem_r02.py): texture address (TA) and data (TD) paths
+    per CU, VALU pipe per SIMD.  Measured on the production kernel in a
+    profiled run, not live; null when no pass was kept."""
+    path = os.path.join(REPO, "profiles", f"units_{cfg.lower()}.json")
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
+
+
 # ---- CPU baseline -------------------------------------------------------------
 def cpu_info() -> dict:
     model = None
@@ -353,7 +366,8 @@ def main():
         loads = executed_loads(exec_counts)
         load_bytes = sum(w * n for w, n in loads.items())
         lds_bytes = 32 * exec_counts["node_visits_lds"]        # fp16 node rows from the LDS copy
-        store_bytes = 16 * own_paths + (32 * owned if mesh else 0)
+        # 12-B path radiances, the 4-B depth term per pixel, the 32-B primary records
+        store_bytes = 12 * own_paths + 4 * owned + (32 * owned if mesh else 0)
         ref_b = reference_bytes(ref_counts, own_paths, owned * F)
         achieved = load_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         roofs = {}
@@ -381,6 +395,7 @@ def main():
                     "lds_node_bytes_per_launch": int(lds_bytes), "store_bytes_per_launch": int(store_bytes),
                     "roofs": roofs,
                     "traffic_source": traffic_src,
+                    "unit_busy": unit_busy(CFG),
                     "vmem_roof_lane_loads_per_ns": ({f"b{8 * w}": v["by_distinct"] for w, v in roof.items()}
                                                     if roof else None),
                     "reference_algorithm": {

@@ -18,6 +18,7 @@ excluded).  Derived figures (per CU, over the kernel's cycles):
 """
 import csv
 import glob
+import json
 import os
 import re
 import sys
@@ -94,6 +95,15 @@ def main():
                 lines.append(f"- {label} wave-instructions per path: {m[k] / paths:.2f}")
     out = os.path.join(REPO, "profiles", f"{name}_mem.md")
     open(out, "w").write("\n".join(lines) + "\n")
+    if g:   # unit busy fractions for bench.py's roofline.unit_busy
+        cyc = g / 8.0
+        units = {"source": os.path.relpath(out, REPO)}
+        for k, key in (("TD_TD_BUSY_sum", "td"), ("TA_TA_BUSY_sum", "ta")):
+            if k in m:
+                units[key] = round(m[k] / (CUS * cyc), 4)
+        if "SQ_INSTS_VALU" in m:
+            units["valu"] = round(m["SQ_INSTS_VALU"] * 2 / (4 * CUS * cyc), 4)
+        json.dump(units, open(os.path.join(REPO, "profiles", f"units_{cfg.lower()}.json"), "w"), indent=1)
     print("\n".join(lines))
 
 

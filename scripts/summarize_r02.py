@@ -129,7 +129,7 @@ def main():
                       f"2*FETCH + WRITE = {traffic / 1e6:.1f} MB = {traffic / 1e9 / (launch_ms / 1e3):.1f} GB/s "
                       f"over the launch ({traffic / 1e9 / (launch_ms / 1e3) / 8000:.4f} of 8 TB/s)")
             if paths:
-                md.append(f"; WRITE_SIZE / (16 B x {paths} path results) = {write * 1024 / (16 * paths):.3f}")
+                md.append(f"; WRITE_SIZE / (12 B x {paths} path results) = {write * 1024 / (12 * paths):.3f} (12-B radiances since r02e; 16-B float4 before)")
             md.append(".\n")
         unprof = bench_line(os.path.join(src, f"bench_{cfg}.log"))
         for tag, b in (("unprofiled bench.py", unprof), ("profiled bench.py", traced_bench)):
