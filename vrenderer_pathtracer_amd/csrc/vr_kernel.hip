@@ -1163,8 +1163,14 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
             muleq4(ps.mask, h.spec);
             newdir = normalize4(sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d))));
         } else {
-            const float rand1 = 2.f * VR_PI * ps.rng.uniform();
-            const float rand2 = ps.rng.uniform();
+            float rand1 = 2.f * VR_PI * ps.rng.uniform();
+            float rand2 = ps.rng.uniform();
+#ifdef VR_PROBE_COHERENT
+            // probe only (invalid images): every lane shading in this step
+            // takes the first lane's direction sample -- the coherence bound
+            rand1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rand1)));
+            rand2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rand2)));
+#endif
             const float rand2s = sqrt_exact(rand2);
             const vr4 u = normalize4(cross4(axis, w));
             const vr4 v = cross4(w, u);
@@ -1181,8 +1187,12 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
     } else if (h.type == 2) {                                            // :724-764
         const vr4 w = normal;
         const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
-        const float rand1 = 2.f * VR_PI * ps.rng.uniform();
-        const float rand2 = ps.rng.uniform();
+        float rand1 = 2.f * VR_PI * ps.rng.uniform();
+        float rand2 = ps.rng.uniform();
+#ifdef VR_PROBE_COHERENT
+        rand1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rand1)));
+        rand2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rand2)));
+#endif
         const float rand2s = sqrt_exact(rand2);
         const vr4 u = normalize4(cross4(axis, w));
         const vr4 v = cross4(w, u);
