@@ -44,6 +44,15 @@ def test_create_without_device_fails_loudly(native):
     assert b"device" in native.vrhip_last_error().lower()
 
 
+def test_create_rejects_bad_sizes(native):
+    """Sizes are checked before any device call: 0 and > 65535 pixels per side
+    (path-kernel pixel coordinates are 16-bit) are VRHIP_ERR_INVALID."""
+    for w, h in ((0, 64), (64, 0), (65536, 64), (64, 70000)):
+        ctx = ctypes.c_void_p()
+        assert native.vrhip_create(0, w, h, ctypes.byref(ctx)) == -1 and not ctx.value
+        assert b"create" in native.vrhip_last_error().lower()
+
+
 def test_null_context_is_invalid(native):
     assert native.vrhip_clear(None) == -1
     assert native.vrhip_render(None, 1, None, 0) == -1
