@@ -1128,11 +1128,12 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // Without overlap every launch uses the same path stream, so it waits
         // for the previous one (and its finish pass, below) like a single stream.
         const bool small = (size_t)p.path_stride * 2u * k < ((size_t)1 << 24);
-        // automatic overlap only behind a launch still in flight: a launch
-        // submitted to an idle device (one frame per synchronous call) runs
-        // its render and finish kernels on `stream` with no cross-stream waits
-        const bool ovl = c->overlap > 0 ||
-                         (c->overlap < 0 && small && c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
+        // automatic overlap only behind a launch still in flight (this call's
+        // previous launch, or the last call's): a launch submitted to an idle
+        // device (one frame per synchronous call) runs its render and finish
+        // kernels on `stream` with no cross-stream waits
+        const bool in_flight = done > 0 || (c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
+        const bool ovl = c->overlap > 0 || (c->overlap < 0 && small && in_flight);
         p.small_blocks = small ? 1u : 0u;
         p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
         p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? VR_QUEUES : VR_QUEUES_LARGE;
