@@ -23,6 +23,7 @@ sc = scenes.make_scene({cfg!r})
 r = VRendererHIP(0)
 scenes.load_into(r, sc)
 r.set_strict_traversal({strict})
+if {overlap!r} != "": r.set_overlap(int({overlap!r}))
 F = {frames}
 r.render(frames=F, time_seed=sc["time"])     # warm-up
 r.clearBuffer()
@@ -52,16 +53,18 @@ def main():
     ap.add_argument("--strict", action="store_true")
     ap.add_argument("--leaf", type=int, default=None, help="max triangles per leaf of the scene's BVH")
     ap.add_argument("--node-cost", type=float, default=None, help="SAH node cost of the scene's BVH")
+    ap.add_argument("--overlap", default="", help="comma-separated vrhip_set_overlap modes to run per library (1, 0, -1)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     results = {}
-    for lib in a.libs:
+    runs = [(lib, ov) for lib in a.libs for ov in (a.overlap.split(",") if a.overlap else [""])]
+    for lib, ov in runs:
         env = dict(os.environ, VRHIP_LIB=os.path.abspath(lib))
         if a.leaf:
             env["VRHIP_MAX_LEAF"] = str(a.leaf)
         if a.node_cost is not None:
             env["VRHIP_SAH_NODE_COST"] = str(a.node_cost)
-        code = CHILD.format(repo=REPO, cfg=a.cfg, frames=a.frames, steps=a.steps, strict=a.strict)
+        code = CHILD.format(repo=REPO, cfg=a.cfg, frames=a.frames, steps=a.steps, strict=a.strict, overlap=ov)
         p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
         if p.returncode != 0:
             print(f"{lib}: FAILED rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
@@ -69,8 +72,9 @@ def main():
                 sys.exit(p.returncode if p.returncode > 0 else 1)
             continue
         res = json.loads(p.stdout.strip().splitlines()[-1])
-        results[lib] = res
-        print(f"{os.path.basename(lib):40s} {res['mpaths']:9.1f} Mpaths/s (best {res['best']:.1f})  hash {res['hash']:#x}",
+        name = os.path.basename(lib) + (f" overlap={ov}" if ov else "")
+        results[name] = res
+        print(f"{name:40s} {res['mpaths']:9.1f} Mpaths/s (best {res['best']:.1f})  hash {res['hash']:#x}",
               flush=True)
     hashes = {v["hash"] for v in results.values()}
     print("all results identical" if len(hashes) == 1 else f"RESULTS DIFFER: {len(hashes)} distinct hashes")
