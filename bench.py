@@ -201,8 +201,8 @@ def cpu_baseline(scene: dict, budget_s: float) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames-per-step", type=int, default=None,
                     help="frames accumulated per step (= per gather); default 16 x N: every GPU renders 16 "
                          "full-frame equivalents per step whatever N (weak scaling in samples, fixed resolution)")

@@ -740,6 +740,14 @@ __device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Tr
 #define VR_NODE_BREAK 6    // measured (path kernel with paired triangle loads): 0 (the reference's
                            // all-lanes vote) C2 2,294, 2: 2,503, 4: 2,563, 6: 2,577, 8: 2,583 (C3 -2 %)
 #endif
+#ifndef VR_NODE_BREAK_CORNELL
+// Cornell-box kernels (every bounce ray stays inside the box and most lanes
+// keep traversing the mesh): r02 6-wave kernel, C2 6: 3,910, 10: 3,986;
+// the HDRI scenes lose at 10 (C3 -1.3 %, C5 -1.2 %) and keep VR_NODE_BREAK
+#define VR_NODE_BREAK_CORNELL 10
+#endif
+template <uint32_t FEAT>
+constexpr int node_break() { return ((FEAT & F_EXACT) && (FEAT & F_CORNELL)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK; }
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
@@ -757,7 +765,7 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         }
         // the wave moves on to the leaves once (nearly) every lane holds one;
         // lanes still searching resume in the next outer iteration
-        if (__popcll(__ballot(leafAddr >= 0)) <= VR_NODE_BREAK) break;
+        if (__popcll(__ballot(leafAddr >= 0)) <= node_break<FEAT>()) break;
     }
     while (leafAddr < 0) {
         const int lv = ~leafAddr;
