@@ -168,6 +168,31 @@ def test_random_soup_bvh_equals_brute_force(oracle):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def test_spatial_split_bvh_equals_brute_force(oracle, monkeypatch):
+    """The opt-in spatial-split builder (VRHIP_SBVH_ALPHA, vr_bvh.cpp
+    SpatialBuilder): a triangle split across leaves is still found wherever a
+    ray meets it -- traversal == testing every triangle, on a soup of large
+    overlapping triangles where splits do happen."""
+    rng = np.random.default_rng(11)
+    n = 200
+    c = rng.uniform(-30, 30, (n, 1, 3))
+    P = (c + rng.normal(0, 12, (n, 3, 3))).reshape(-1, 3).astype(np.float32)
+    m = dict(positions=P, normals=np.tile([0, 0, 1], (3 * n, 1)).astype(np.float32),
+             tangents=np.tile([1, 0, 0], (3 * n, 1)).astype(np.float32),
+             uvs=rng.uniform(0, 1, (3 * n, 2)).astype(np.float32),
+             tris=np.arange(3 * n, dtype=np.uint32).reshape(-1, 3))
+    plain = build_flat(m, max_leaf_tris=2)
+    monkeypatch.setenv("VRHIP_SBVH_ALPHA", "1e-5")
+    split = build_flat(m, max_leaf_tris=2)
+    validate_flat(split)
+    assert len(split["verts"]) > len(plain["verts"])          # references were split
+    sc = scenes.make_scene("C2", 48, 32)
+    sc["mesh_flat"] = split
+    a, _, _, _ = po.render(sc, frames=1)
+    b, _, _, _ = po.render(sc, frames=1, brute_force=True)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 @pytest.mark.parametrize("W,H,n", [(1280, 720, 1), (1280, 720, 2), (1280, 720, 8), (1920, 1080, 8), (64, 40, 3),
                                    (40, 15, 2), (48, 48, 16)])
 def test_tile_pixels_partition(native, W, H, n):

@@ -71,6 +71,9 @@ struct Builder {
 #ifndef VR_BVH_NODE_COST
 #define VR_BVH_NODE_COST 1.0
 #endif
+#ifndef VR_BVH_SBVH_ALPHA
+#define VR_BVH_SBVH_ALPHA 0.0      // spatial splits off (VRHIP_SBVH_ALPHA > 0 enables them)
+#endif
     static constexpr int kBins = VR_BVH_BINS;
     static constexpr uint32_t kParallelTask = 16384;    // subtrees at least this big may get a thread
     static constexpr uint32_t kParallelBin = 131072;    // nodes at least this big bin in parallel
@@ -216,6 +219,202 @@ struct Builder {
     }
 };
 
+// Spatial-split SAH (SBVH, Stich et al. 2009 -- the tree family the
+// reference application builds, src/SBVH.cpp): a node may split a triangle
+// reference at a plane instead of partitioning whole triangles; each piece
+// keeps the triangle id and a box clipped to its side.  Single-threaded and
+// deterministic; used when VRHIP_SBVH_ALPHA > 0 (the overlap threshold of
+// the object split, relative to the root's area, above which spatial splits
+// are tried).  Leaves list triangle ids (a split triangle appears in several
+// leaves: the kernel's equal-t tie-break keeps one copy, and the copies carry
+// the same attributes, so the image is unchanged).
+struct SpatialBuilder {
+    struct Ref { uint32_t tri; Box box; };
+    const float* pos;
+    const uint32_t* tris;
+    uint32_t max_leaf = 2, max_depth = kMaxBuildDepth;
+    double node_cost = 1.0, min_overlap = 0.0;
+    size_t ref_budget = 0;               // spatial splits stop when the references reach this
+    size_t n_refs = 0;
+    std::vector<BuildNode> nodes;
+    std::vector<uint32_t> leaf_tris;
+    static constexpr int kObjBins = 64, kSpatialBins = 32;
+
+    const float* vtx(uint32_t t, int k) const { return &pos[3 * (size_t)tris[3 * (size_t)t + k]]; }
+
+    int make_leaf(const std::vector<Ref>& refs, const Box& b) {
+        BuildNode n; n.box = b; n.leaf = true;
+        n.first = (uint32_t)leaf_tris.size(); n.count = (uint32_t)refs.size();
+        for (const Ref& r : refs) leaf_tris.push_back(r.tri);
+        nodes.push_back(n);
+        return (int)nodes.size() - 1;
+    }
+    // the parts of triangle r.tri within r.box on either side of the plane
+    // x[a] = p, each clipped to r.box; intersection points in double, the
+    // boxes rounded outward (a piece box must contain its piece)
+    void split_ref(const Ref& r, int a, float p, Ref& L, Ref& R) const {
+        L.tri = R.tri = r.tri; L.box = Box(); R.box = Box();
+        auto grow_out = [](Box& b, const double* q) {
+            for (int i = 0; i < 3; ++i) {
+                const float f = (float)q[i];
+                b.lo[i] = std::min(b.lo[i], (double)f > q[i] ? std::nextafter(f, -INFINITY) : f);
+                b.hi[i] = std::max(b.hi[i], (double)f < q[i] ? std::nextafter(f, INFINITY) : f);
+            }
+        };
+        for (int e = 0; e < 3; ++e) {
+            const float* v0 = vtx(r.tri, e);
+            const float* v1 = vtx(r.tri, (e + 1) % 3);
+            const double q0[3] = { v0[0], v0[1], v0[2] };
+            if (v0[a] <= p) grow_out(L.box, q0);
+            if (v0[a] >= p) grow_out(R.box, q0);
+            if ((v0[a] < p && v1[a] > p) || (v0[a] > p && v1[a] < p)) {
+                const double t = ((double)p - v0[a]) / ((double)v1[a] - v0[a]);
+                double q[3];
+                for (int i = 0; i < 3; ++i) q[i] = (double)v0[i] + t * ((double)v1[i] - v0[i]);
+                q[a] = p;
+                grow_out(L.box, q);
+                grow_out(R.box, q);
+            }
+        }
+        for (int i = 0; i < 3; ++i) {
+            L.box.lo[i] = std::max(L.box.lo[i], r.box.lo[i]); L.box.hi[i] = std::min(L.box.hi[i], r.box.hi[i]);
+            R.box.lo[i] = std::max(R.box.lo[i], r.box.lo[i]); R.box.hi[i] = std::min(R.box.hi[i], r.box.hi[i]);
+        }
+        L.box.hi[a] = std::min(L.box.hi[a], p);
+        R.box.lo[a] = std::max(R.box.lo[a], p);
+    }
+    static Box overlap(const Box& x, const Box& y) {
+        Box o;
+        for (int i = 0; i < 3; ++i) { o.lo[i] = std::max(x.lo[i], y.lo[i]); o.hi[i] = std::min(x.hi[i], y.hi[i]); }
+        for (int i = 0; i < 3; ++i) if (o.lo[i] > o.hi[i]) return Box();
+        return o;
+    }
+
+    int build(std::vector<Ref>& refs, uint32_t depth, bool force_split) {
+        Box b, cb;
+        for (const Ref& r : refs) {
+            b.grow(r.box);
+            const float c[3] = { 0.5f * (r.box.lo[0] + r.box.hi[0]), 0.5f * (r.box.lo[1] + r.box.hi[1]),
+                                 0.5f * (r.box.lo[2] + r.box.hi[2]) };
+            cb.grow(c);
+        }
+        const uint32_t count = (uint32_t)refs.size();
+        if (!force_split && (count <= 1 || depth + 1 >= max_depth)) return make_leaf(refs, b);
+        auto cent = [&](const Ref& r, int a) { return 0.5f * (r.box.lo[a] + r.box.hi[a]); };
+        // object split: binned SAH over the references' centroids
+        double obj_cost = INFINITY; int obj_axis = -1, obj_split = -1; Box obj_l, obj_r;
+        for (int a = 0; a < 3; ++a) {
+            const float ext = cb.hi[a] - cb.lo[a];
+            if (!(ext > 0.f)) continue;
+            const double scale = kObjBins / (double)ext;
+            Box bb[kObjBins]; uint32_t bc[kObjBins] = {};
+            for (const Ref& r : refs) {
+                int k = std::min(std::max((int)(((double)cent(r, a) - cb.lo[a]) * scale), 0), kObjBins - 1);
+                bc[k]++; bb[k].grow(r.box);
+            }
+            Box rb[kObjBins]; uint32_t rc[kObjBins];
+            Box acc; uint32_t c = 0;
+            for (int k = kObjBins - 1; k > 0; --k) { acc.grow(bb[k]); c += bc[k]; rb[k] = acc; rc[k] = c; }
+            acc = Box(); c = 0;
+            for (int k = 0; k < kObjBins - 1; ++k) {
+                acc.grow(bb[k]); c += bc[k];
+                if (c == 0 || rc[k + 1] == 0) continue;
+                const double cost = acc.area() * c + rb[k + 1].area() * rc[k + 1];
+                if (cost < obj_cost) { obj_cost = cost; obj_axis = a; obj_split = k; obj_l = acc; obj_r = rb[k + 1]; }
+            }
+        }
+        // spatial split: reference pieces chopped into bins over the node box
+        double sp_cost = INFINITY; int sp_axis = -1; float sp_pos = 0.f;
+        if (n_refs < ref_budget && obj_axis >= 0 && overlap(obj_l, obj_r).area() > min_overlap) {
+            for (int a = 0; a < 3; ++a) {
+                const float ext = b.hi[a] - b.lo[a];
+                if (!(ext > 0.f)) continue;
+                float plane[kSpatialBins + 1];
+                for (int k = 0; k <= kSpatialBins; ++k) plane[k] = b.lo[a] + ext * ((float)k / kSpatialBins);
+                plane[kSpatialBins] = b.hi[a];
+                auto bin_of = [&](float x) {
+                    int k = (int)(((double)x - b.lo[a]) / (double)ext * kSpatialBins);
+                    return std::min(std::max(k, 0), kSpatialBins - 1);
+                };
+                Box bb[kSpatialBins]; uint32_t enter[kSpatialBins] = {}, exit_[kSpatialBins] = {};
+                for (const Ref& r : refs) {
+                    const int k0 = bin_of(r.box.lo[a]), k1 = bin_of(r.box.hi[a]);
+                    enter[k0]++; exit_[k1]++;
+                    Ref cur = r;
+                    for (int k = k0; k < k1; ++k) {
+                        Ref lp, rp;
+                        split_ref(cur, a, plane[k + 1], lp, rp);
+                        if (!lp.box.empty()) bb[k].grow(lp.box);
+                        cur = rp;
+                    }
+                    if (!cur.box.empty()) bb[k1].grow(cur.box);
+                }
+                Box rb[kSpatialBins]; uint32_t rc[kSpatialBins];
+                Box acc; uint32_t c = 0;
+                for (int k = kSpatialBins - 1; k > 0; --k) { acc.grow(bb[k]); c += exit_[k]; rb[k] = acc; rc[k] = c; }
+                acc = Box(); c = 0;
+                for (int k = 0; k < kSpatialBins - 1; ++k) {
+                    acc.grow(bb[k]); c += enter[k];
+                    if (c == 0 || rc[k + 1] == 0) continue;
+                    const double cost = acc.area() * c + rb[k + 1].area() * rc[k + 1];
+                    if (cost < sp_cost) { sp_cost = cost; sp_axis = a; sp_pos = plane[k + 1]; }
+                }
+            }
+        }
+        const double parent_area = b.area();
+        const double best = std::min(obj_cost, sp_cost);
+        const double split_cost = node_cost + (parent_area > 0.0 ? best / parent_area : (double)count);
+        const bool want_leaf = count <= max_leaf && (obj_axis < 0 || split_cost >= (double)count);
+        if (!force_split && want_leaf) return make_leaf(refs, b);
+
+        std::vector<Ref> left, right;
+        if (sp_axis >= 0 && sp_cost < obj_cost) {
+            const int a = sp_axis;
+            for (const Ref& r : refs) {
+                if (r.box.hi[a] <= sp_pos && !(r.box.lo[a] == sp_pos)) left.push_back(r);
+                else if (r.box.lo[a] >= sp_pos) right.push_back(r);
+                else {
+                    Ref lp, rp;
+                    split_ref(r, a, sp_pos, lp, rp);
+                    if (!lp.box.empty()) left.push_back(lp);
+                    if (!rp.box.empty()) right.push_back(rp);
+                    if (!lp.box.empty() && !rp.box.empty()) ++n_refs;
+                }
+            }
+            if (left.empty() || right.empty() || left.size() == count && right.size() == count) {
+                left.clear(); right.clear();
+                sp_axis = -1;
+            }
+        }
+        if (left.empty() && right.empty()) {
+            if (obj_axis >= 0) {
+                const int a = obj_axis;
+                const double scale = kObjBins / (double)(cb.hi[a] - cb.lo[a]);
+                for (const Ref& r : refs) {
+                    int k = std::min(std::max((int)(((double)cent(r, a) - cb.lo[a]) * scale), 0), kObjBins - 1);
+                    (k <= obj_split ? left : right).push_back(r);
+                }
+            }
+            if (left.empty() || right.empty()) {       // coincident centroids: halves by order
+                left.assign(refs.begin(), refs.begin() + count / 2);
+                right.assign(refs.begin() + count / 2, refs.end());
+            }
+        }
+        std::vector<Ref>().swap(refs);
+        int l, r;
+        if (count == 1) {                              // forced split of one triangle (see Builder::build)
+            l = make_leaf(right.empty() ? left : right, b);
+            r = make_leaf(right.empty() ? left : right, b);
+        } else {
+            l = build(left, depth + 1, false);
+            r = build(right, depth + 1, false);
+        }
+        BuildNode n; n.box = b; n.child[0] = l; n.child[1] = r; n.leaf = false;
+        nodes.push_back(n);
+        return (int)nodes.size() - 1;
+    }
+};
+
 // Host threads for the builder: VRHIP_BUILD_THREADS, else OMP_NUM_THREADS,
 // else the machine's concurrency, at most 16.
 int build_threads()
@@ -265,9 +464,28 @@ int build_flat(const float* positions, const float* normals, const float* tangen
         for (int a = 0; a < 3; ++a) B.centroid[3 * (size_t)t + a] = 0.5f * (bx.lo[a] + bx.hi[a]);
         B.refs[t] = t;
     }
-    B.nodes.resize(2 * (size_t)n_tris + 2);
-    B.spare_threads = build_threads() - 1;
-    const int root = B.build(0, n_tris, 0, true);
+    double sbvh_alpha = VR_BVH_SBVH_ALPHA;
+    if (const char* e = std::getenv("VRHIP_SBVH_ALPHA")) sbvh_alpha = std::atof(e);
+    int root;
+    if (sbvh_alpha > 0.0) {
+        SpatialBuilder S;
+        S.pos = positions; S.tris = tris; S.max_leaf = B.max_leaf; S.node_cost = B.node_cost;
+        S.max_depth = kMaxBuildDepth;
+        S.n_refs = n_tris;
+        S.ref_budget = (size_t)n_tris + n_tris / 2;     // at most 50 % more references
+        std::vector<SpatialBuilder::Ref> refs(n_tris);
+        Box all;
+        for (uint32_t t = 0; t < n_tris; ++t) { refs[t] = { t, B.tri_box[t] }; all.grow(B.tri_box[t]); }
+        S.min_overlap = sbvh_alpha * all.area();
+        S.nodes.reserve(4 * (size_t)n_tris + 2);
+        root = S.build(refs, 0, true);
+        B.nodes = std::move(S.nodes);
+        B.refs = std::move(S.leaf_tris);
+    } else {
+        B.nodes.resize(2 * (size_t)n_tris + 2);
+        B.spare_threads = build_threads() - 1;
+        root = B.build(0, n_tris, 0, true);
+    }
 
     // Flatten (reference: explicit-stack DFS, src/vRendererCuda.cpp:204-279)
     out.bvh.assign(4, vr4{ 0.f, 0.f, 0.f, 0.f });
