@@ -376,6 +376,19 @@ def main():
             roofs["vmem"] = {"achieved": round(achieved, 1), "peak": round(load_bytes / t_min / 1e9, 1),
                              "frac": round(t_min / avg_launch_s, 4)}
         roofs["l2"] = {"achieved": round(achieved, 1), "peak": L2_PEAK_GBS, "frac": round(achieved / L2_PEAK_GBS, 4)}
+        # where the kernel's gather rate sits between the micro-benchmark's
+        # one-address-per-wave roof and its 64-distinct-lines rate (every lane
+        # on its own line): not a roof, a position -- the texture path charges
+        # per line a lane touches, so divergent rays sit near the second figure
+        gpos = None
+        if roof and load_bytes > 0:
+            def rate(w, d):                          # lane loads per second
+                return roof[w]["by_distinct"][str(d)] * 1e9
+            t_div = sum(n / rate(w, 64) for w, n in loads.items() if n)
+            t_one = sum(n / rate(w, 1) for w, n in loads.items() if n)
+            gpos = {"launch_ms": round(avg_launch_s * 1e3, 4), "ms_at_1_address": round(t_one * 1e3, 4),
+                      "ms_at_64_lines": round(t_div * 1e3, 4),
+                      "lane_loads_per_ns": round(sum(loads.values()) / avg_launch_s / 1e9, 1)}
         traffic, traffic_src = hbm_traffic(CFG)
         if traffic and world == 1:
             hbm_gbs = traffic / avg_launch_s / 1e9
@@ -394,6 +407,7 @@ def main():
                     "lane_loads_per_launch": {f"b{8 * w}": int(n) for w, n in loads.items()},
                     "lds_node_bytes_per_launch": int(lds_bytes), "store_bytes_per_launch": int(store_bytes),
                     "roofs": roofs,
+                    "gather_position": gpos,
                     "traffic_source": traffic_src,
                     "unit_busy": unit_busy(CFG),
                     "vmem_roof_lane_loads_per_ns": ({f"b{8 * w}": v["by_distinct"] for w, v in roof.items()}

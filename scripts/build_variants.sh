@@ -11,7 +11,7 @@ for spec in "$@"; do
   ( rm -f variants/libvrhip_$name.so
     hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -shared -pthread --offload-arch=gfx950 -Xclang -target-feature -Xclang -packed-fp32-ops $flags \
       -o variants/libvrhip_$name.so $SRC -Rpass-analysis=kernel-resource-usage > variants/$name.log 2>&1
-    grep -E -A12 "render_wave_kernelILi16ELj2147483657ELi768E" variants/$name.log | grep -E "VGPRs:|VGPRs Spill|Scratch" \
+    grep -E -A12 "render_wave_kernelILi16ELj2147483657ELi[0-9]+E" variants/$name.log | grep -E "VGPRs:|VGPRs Spill|Scratch" \
       | sed 's/.*remark: *//;s/ \[-Rpass.*//' | tr '\n' ' ' | sed "s/^/$name: /"; echo
     [ -f variants/libvrhip_$name.so ] || { grep -m5 error: variants/$name.log; echo "$name: BUILD FAILED"; } ) &
 done

@@ -443,8 +443,9 @@ def test_stack24_tree_bitexact_vs_portable_oracle(native, oracle, cfg):
 @pytest.mark.parametrize("cfg", ["C2", "C3"])
 def test_large_and_small_launch_blocks_agree(native, cfg):
     """A 20-frame 1280x720 launch (36.9 M paths) runs the path kernel in
-    768-thread blocks on 64 queue heads, one frame per call (1.8 M paths) in
-    256-thread blocks on 16: the accumulations are identical bit for bit."""
+    768-thread blocks (C3; C2's Cornell kernel: 256-thread blocks at 7 waves)
+    on 64 queue heads, one frame per call (1.8 M paths) in 256-thread blocks on
+    16: the accumulations are identical bit for bit."""
     sc = scenes.make_scene(cfg)
     times = [sc["time"] + i for i in range(20)]
     big, _, _, n_big = gpu_render(sc, 20, times)

@@ -747,7 +747,11 @@ __device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Tr
 #define VR_NODE_BREAK_CORNELL 10
 #endif
 template <uint32_t FEAT>
-constexpr int node_break() { return ((FEAT & F_EXACT) && (FEAT & F_CORNELL)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK; }
+constexpr int node_break() {
+    // one-frame kernels (F_INLINE_PRIM) keep 6: the interactive C2 rate fell
+    // 2,147 -> 2,103 Mpaths/s with 10 (r02h)
+    return ((FEAT & F_EXACT) && (FEAT & F_CORNELL) && !(FEAT & F_INLINE_PRIM)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK;
+}
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
@@ -1545,20 +1549,44 @@ enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3, LS_
 #endif
 static_assert(VR_PATH_BLOCK % kBlockThreads == 0, "VR_PATH_BLOCK must be a multiple of 256");
 static_assert((4 * VR_PATH_WAVES * 64) % VR_PATH_BLOCK == 0, "whole blocks per CU");
-constexpr int wave_block(int stack) { return stack <= kQ4Stack ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads; }
+// Cornell-box mesh kernels with 16-entry stacks (C2) run 7 waves per SIMD in
+// 256-thread blocks (72 VGPRs, SGPR spills only): C2 3,991 -> 4,109 Mpaths/s,
+// while the HDRI scenes lose with it (C3 -2 %, C5 -17 %: their longer shading
+// code spills) and keep VR_PATH_WAVES in VR_PATH_BLOCK-thread blocks.
+#ifndef VR_PATH_WAVES_CORNELL
+#define VR_PATH_WAVES_CORNELL 7
+#endif
+#ifndef VR_PATH_BLOCK_CORNELL
+#define VR_PATH_BLOCK_CORNELL 256
+#endif
+static_assert(VR_PATH_BLOCK_CORNELL % kBlockThreads == 0, "VR_PATH_BLOCK_CORNELL must be a multiple of 256");
+static_assert((4 * VR_PATH_WAVES_CORNELL * 64) % VR_PATH_BLOCK_CORNELL == 0, "whole blocks per CU");
+// c: the kernel is a Cornell-box specialisation (cornell_kernel<FEAT>())
+constexpr bool cornell_res(int stack, bool c) { return c && stack <= 16; }
+constexpr int wave_block(int stack, bool c) {
+    return cornell_res(stack, c) ? VR_PATH_BLOCK_CORNELL : stack <= kQ4Stack ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads;
+}
 // Launches of fewer than 2^24 paths (sharded frames, RenderParams::small_blocks)
 // take 256-thread blocks at the same residency: a block frees its CU slot once
 // its 4 waves are done rather than 12, so the launch's drain overlaps the next
 // launch sooner.  Projected 8-rank C2 step 1.283 -> 1.193 ms (C3 0.468 ->
 // 0.420 ms), while whole frames keep the 768-thread blocks (C2 3,437 vs 3,244).
-constexpr int wave_block_small(int stack) { return stack <= kQ4Stack ? kBlockThreads : wave_block(stack); }
-constexpr int path_waves(int stack) { return stack <= kQ4Stack ? VR_PATH_WAVES : stack <= 32 ? 4 : 2; }
-constexpr int path_blocks_per_cu(int stack, int bt) { return 4 * path_waves(stack) * 64 / bt; }
+constexpr int wave_block_small(int stack, bool c) { return stack <= kQ4Stack ? kBlockThreads : wave_block(stack, c); }
+constexpr int path_waves(int stack, bool c) {
+    return cornell_res(stack, c) ? VR_PATH_WAVES_CORNELL : stack <= kQ4Stack ? VR_PATH_WAVES : stack <= 32 ? 4 : 2;
+}
+constexpr int path_blocks_per_cu(int stack, int bt, bool c) { return 4 * path_waves(stack, c) * 64 / bt; }
 // LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
 // the node cache takes what the stacks leave (56 B per node)
-constexpr int path_cache_nodes(int stack, int bt) {
-    return (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)) / 56 > 0
-               ? (163840 / path_blocks_per_cu(stack, bt) - bt - stack * bt * stack_entry_bytes(stack)) / 56 : 1;
+constexpr int path_cache_nodes(int stack, int bt, bool c) {
+    return (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * stack_entry_bytes(stack)) / 56 > 0
+               ? (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * stack_entry_bytes(stack)) / 56 : 1;
+}
+template <uint32_t FEAT>
+constexpr bool cornell_kernel() {
+    // the one-frame kernels (F_INLINE_PRIM) keep 6 waves: at 7 the interactive
+    // C2 rate fell 2,147 -> 2,100 Mpaths/s (r02g)
+    return (FEAT & F_EXACT) != 0u && (FEAT & F_CORNELL) != 0u && (FEAT & F_INLINE_PRIM) == 0u;
 }
 
 #ifndef VR_XCD_BANDS
@@ -1581,9 +1609,9 @@ __device__ __forceinline__ void sub_pixel(const RenderParams& p, uint32_t sub, u
 }
 
 template <int STACK, uint32_t FEAT, int BT>
-__global__ void __launch_bounds__(BT, path_waves(STACK)) render_wave_kernel(const RenderParams p)
+__global__ void __launch_bounds__(BT, path_waves(STACK, cornell_kernel<FEAT>())) render_wave_kernel(const RenderParams p)
 {
-    constexpr int CN = path_cache_nodes(STACK, BT);
+    constexpr int CN = path_cache_nodes(STACK, BT, cornell_kernel<FEAT>());
     __shared__ int lds_stack[STACK * BT];
     __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * BT : 1];
     __shared__ vr4 lds_nodes[3 * CN];
@@ -1921,14 +1949,15 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
         if (p.inline_prim) { launch_wave<STACK, FEAT | F_INLINE_PRIM>(p, n_tiles, s); return; }
         hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
     }
-    // one resident set: path_waves(STACK) waves per SIMD, 4 SIMDs per CU
-    constexpr int BT = wave_block(STACK), BTS = wave_block_small(STACK);
+    // one resident set: path_waves(STACK, C) waves per SIMD, 4 SIMDs per CU
+    constexpr bool C = cornell_kernel<FEAT>();
+    constexpr int BT = wave_block(STACK, C), BTS = wave_block_small(STACK, C);
     if (BTS != BT && p.small_blocks) {
-        hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * path_blocks_per_cu(STACK, BTS)),
+        hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * path_blocks_per_cu(STACK, BTS, C)),
                            dim3(BTS), 0, s, p);
         return;
     }
-    constexpr uint32_t per_cu = (uint32_t)path_blocks_per_cu(STACK, BT);
+    constexpr uint32_t per_cu = (uint32_t)path_blocks_per_cu(STACK, BT, C);
     hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BT>), dim3(p.wave_blocks * per_cu),
                        dim3(BT), 0, s, p);
 }
