@@ -6,6 +6,7 @@
 // GPU, status codes instead of exit(0) (src/vRendererCuda.cpp:454-467), flags
 // passed by value in the launch instead of __constant__ symbol copies
 // (cuda/src/PathTracer.cu:976-1001), and multi-frame render steps.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <hip/hip_gl_interop.h>
 #include <rccl/rccl.h>
@@ -1136,7 +1137,15 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         const bool ovl = c->overlap > 0 || (c->overlap < 0 && small && in_flight);
         p.small_blocks = small ? 1u : 0u;
         p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
-        p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? VR_QUEUES : VR_QUEUES_LARGE;
+        p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? (c->cornell ? VR_QUEUES : VR_QUEUES_HDRI)
+                                                                        : VR_QUEUES_LARGE;
+        // VRHIP_QUEUES: work-queue heads for experiments (a power of two, 8..VR_MAX_QUEUES)
+        static const uint32_t env_queues = [] {
+            const char* e = std::getenv("VRHIP_QUEUES");
+            const uint32_t q = e ? (uint32_t)std::atoi(e) : 0u;
+            return (q >= 8 && q <= (uint32_t)VR_MAX_QUEUES && (q & (q - 1)) == 0) ? q : 0u;
+        }();
+        if (env_queues) p.n_queues = env_queues;
         if (!ovl) c->parity = 0;
         auto& l = c->lane[c->parity];
         // overlapped launches run on the lane's path stream, the others on
