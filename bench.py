@@ -56,6 +56,8 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md "HBM": 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate
+# VALU: 256 CUs x 4 SIMDs x 32 lane-ops/cycle (wave64 over 2 cycles) x 2.4 GHz
+VALU_PEAK_TOPS = round(256 * 4 * 32 * 2.4e9 / 1e12, 2)
 METRIC = "Mpaths/sec (+ Mrays/sec) at 1280x720 progressive; 1/2/4/8 MI355X"
 WORKLOADS = {
     "C1": ("C1: Cornell box + example sphere, 512x512, 2 spp/frame, 4 bounces",
@@ -211,6 +213,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--interactive-frames", type=int, default=30,
                     help="frames of the one-frame-per-call measurement (0: skip)")
+    ap.add_argument("--strong-steps", type=int, default=20,
+                    help="steps of the fixed 16-frames-per-step measurement reported under 'strong' (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roof", action="store_true", help="skip the vector-memory roof micro-benchmark")
     ap.add_argument("--check-launch", action="store_true",
@@ -316,6 +320,61 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    wr = (W // 16) * 16
+    hr = (H // 16) * 16
+
+    def timed_steps(rr, frames, steps, base, with_gather=True):
+        """max-over-ranks wall time of `steps` back-to-back steps of `frames`
+        frames on renderer rr (+ the tile gather per step)."""
+        def one(i):
+            rr.render(frames=frames, times=[base + i * frames + k for k in range(frames)], sync=False)
+            if with_gather:
+                gather.step()
+        for i in range(2):
+            one(i)
+        rr.sync()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            one(2 + i)
+        rr.sync()
+        if world > 1:
+            dist.barrier()
+        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    # fixed cadence: 16 frames per step (per gather) whatever N -- the
+    # strong-scaling view of the same job -- against the 1-GPU rate of the
+    # same 16-frame step, measured on every GPU at once over the whole image
+    strong = None
+    if args.strong_steps > 0:
+        SF = 16
+        if F != SF:
+            r.clearBuffer()
+            ts, n_st = timed_steps(r, SF, args.strong_steps, scene["time"] + 500000), args.strong_steps
+        else:
+            ts, n_st = elapsed, args.steps          # the main measurement is already at 16 frames per step
+        strong = {"frames_per_step": SF, "steps": n_st,
+                  "value": round(wr * hr * 2 * SF * n_st / ts / 1e6, 3),
+                  "ms_per_step": round(ts / n_st * 1e3, 4)}
+        if world > 1:
+            # a second context renders the whole image alone on every GPU at once
+            r1 = VRendererHIP(gpu)
+            scenes.load_into(r1, scene)
+            t1 = timed_steps(r1, SF, args.strong_steps, scene["time"] + 600000, with_gather=False)
+            r1.cleanUp()
+            one_gpu = wr * hr * 2 * SF * args.strong_steps / t1 / 1e6
+        else:
+            one_gpu = strong["value"]
+        strong["one_gpu_value"] = round(one_gpu, 3)
+        strong["efficiency"] = round(strong["value"] / (world * one_gpu), 4)
+        strong["note"] = ("16 frames per step and per RCCL gather for any N (fixed display cadence); efficiency = "
+                          "value / (N x one_gpu_value), one_gpu_value = the same 16-frame step over the whole "
+                          "image on one GPU, measured in this run on every GPU at once")
+
     # interactive cadence: one frame per synchronous render() call (+ gather)
     inter = None
     if args.interactive_frames > 0:
@@ -352,13 +411,18 @@ def main():
         dist.all_reduce(cvec)
     tot = {k: float(v) for k, v in zip(keys + ["owned_pixels"], cvec.tolist())}
 
-    wr = (W // 16) * 16
-    hr = (H // 16) * 16
     paths_per_step = wr * hr * 2 * F
     total_paths = paths_per_step * args.steps
     value = total_paths / elapsed / 1e6
     rays_per_path = tot["rays"] / paths_per_step
     mrays = value * rays_per_path
+    # rays the production kernels trace (the instrumented copy's own count:
+    # camera rays once per pixel per launch, shared by its paths, plus every
+    # bounce ray; no material sampling after the last bounce)
+    evec = torch.tensor([float(exec_counts["rays"])], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(evec)
+    rays_per_path_traced = float(evec.item()) / paths_per_step
 
     if rank == 0:
         own_paths = owned * 2 * F
@@ -393,13 +457,22 @@ def main():
         if traffic and world == 1:
             hbm_gbs = traffic / avg_launch_s / 1e9
             roofs["hbm"] = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(hbm_gbs / HBM_PEAK_GBS, 4)}
+        ub = unit_busy(CFG)
+        if load_bytes == 0 and ub and "valu" in ub:
+            # VALU issue roof: a wave64 VALU instruction issues over 2 cycles
+            # (MI355X_MICROARCH.md "CU"), so a SIMD retires at most 32 lane-ops
+            # per cycle; busy fraction from the counter passes of this config
+            roofs["valu"] = {"achieved": round(ub["valu"] * VALU_PEAK_TOPS, 2), "peak": VALU_PEAK_TOPS,
+                             "frac": ub["valu"], "unit": "T VALU lane-ops/s"}
         if load_bytes == 0:
-            # sphere-only scenes (C1): no global loads on the path -- the
-            # kernel is VALU-bound (sphere tests, libm); report the HBM line only
+            # sphere-only scenes without textures (C1): no global loads on the
+            # path -- the sphere tests and libm are VALU work, priced by the
+            # VALU roof above when this config's counter pass is kept
             roofs.pop("l2", None)
             roofs.setdefault("hbm", {"achieved": 0.0, "peak": HBM_PEAK_GBS, "frac": 0.0})
         bound = max(roofs, key=lambda k: roofs[k]["frac"])
-        roofline = {"bound": bound, "achieved": roofs[bound]["achieved"], "peak": roofs[bound]["peak"], "unit": "GB/s",
+        roofline = {"bound": bound, "achieved": roofs[bound]["achieved"], "peak": roofs[bound]["peak"],
+                    "unit": roofs[bound].get("unit", "GB/s"),
                     "frac": roofs[bound]["frac"], "traffic": traffic if world == 1 else None,
                     "kernel": "primary_kernel+render_wave_kernel" if mesh else "render_kernel",
                     "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches": launches,
@@ -442,6 +515,13 @@ def main():
                                   + " of RGBA8 tiles to rank 0 per step") if world > 1 else "none"},
             "mrays_per_s": round(mrays, 3),
             "rays_per_path": round(rays_per_path, 4),
+            "mrays_per_s_traced": round(value * rays_per_path_traced, 3),
+            "rays_per_path_traced": round(rays_per_path_traced, 4),
+            "mrays_note": ("mrays_per_s is reference-equivalent: intersectScene calls of the reference algorithm "
+                           "(two camera rays per pixel per frame, SURVEY 8d) at this path rate; "
+                           "mrays_per_s_traced counts the rays the kernels trace (a pixel's camera ray once "
+                           "per launch: no camera jitter, PathTracer.cu:842-844)"),
+            "strong": strong,
             "interactive": inter,
             "roofline": roofline,
         }

@@ -147,7 +147,8 @@ int vrhip_gl_present(vrhip_ctx *ctx);
  * frame i (the reference uses wall-clock ms); times may be NULL, then
  * `time_seed` is used for every frame.  Enqueues and returns; call
  * vrhip_sync for the reference's synchronous behaviour.  The path kernels
- * run on the context's two internal path streams (see vrhip_set_overlap);
+ * run on the context stream or, behind a launch still in flight, on the
+ * context's three internal path streams (see vrhip_set_overlap);
  * the finish pass that writes the accumulation, colour and depth images runs
  * on the context stream after them, so work queued on the context stream
  * afterwards (reads, vrhip_pack_tiles, a collective) sees the results. */
@@ -163,9 +164,13 @@ int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *time
                          uint64_t counters[8]);
 /* Same render as vrhip_render -- the production kernels' algorithm (t-culled
  * traversal unless strict, primary hit shared by a pixel's paths, last bounce
- * without material sampling), launch shape and results -- through an
- * instrumented instantiation that counts the memory operations those kernels
- * issue (the roofline's executed bytes; no reference counterpart).
+ * without material sampling), the scene specialisation's launch shape
+ * (block size, waves per SIMD, node-loop threshold, work queues) and results
+ * -- through an instrumented instantiation of that specialisation that
+ * counts the memory operations its kernels issue (the roofline's executed
+ * bytes; no reference counterpart).  Launches of one frame take the primary
+ * pass here (production traces their camera rays in the path kernel), and
+ * counting launches never overlap a launch in flight.
  * counters[0..7] as vrhip_render_counted but for the executed work
  * (attribute bytes include the 36 B of vertices a mesh hit's face normal
  * reads), then [8] node visits served from the block's LDS copy of the tree
@@ -212,7 +217,8 @@ int vrhip_device_buffers(vrhip_ctx *ctx, void **accum, void **rgba8, void **dept
  * t % n_ranks == rank: tiles dealt round-robin, so every rank gets the same
  * number of tiles (+-1) spread over the whole image (sky vs mesh balance).
  * Seeds use global pixel coordinates, so the union of the ranks' tiles equals
- * the 1-GPU image bit for bit. */
+ * the 1-GPU image bit for bit.  VRHIP_ERR_INVALID while a communicator
+ * (vrhip_comm_init) with another tiling exists. */
 int vrhip_set_tiling(vrhip_ctx *ctx, uint32_t rank, uint32_t n_ranks);
 /* Host-only (no device): linear pixel indices (y * width + x) that rank
  * `rank` of n_ranks owns, in packed order (owned tile j holds packed pixels

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Memory-pipeline / issue counters of the current production kernel, one
-# counter group per rocprofv3 pass.  Usage: bash scripts/gpu_mem_r02.sh <tag> [config]
+# counter group per rocprofv3 pass.  Usage: bash scripts/gpu_mem.sh <tag> [config]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-mem}; CFG=${2:-C2}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp

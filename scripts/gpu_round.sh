@@ -1,29 +1,35 @@
 #!/bin/bash
-# Full GPU check on the box: parity tests, smoke, bench, rocprofv3 summaries.
-# Usage: bash scripts/gpu_round.sh <tag> [--no-prof]
+# Round GPU pass: parity tests, smoke, bench lines for C1-C5, and for
+# C2/C3/C5 a rocprofv3 kernel trace plus separate FETCH_SIZE / WRITE_SIZE
+# passes of the same bench command.  Usage: bash scripts/gpu_round.sh <tag> [--no-tests]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-TAG=${1:-r01}
-OUT=gpurun_out/round_$TAG
+TAG=${1:-r02}
+OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 
-step() {  # step <name> <timeout> <cmd...>; stops the script on a crash/timeout
+step() {  # step <name> <timeout> <cmd...>; stops the script on a crash / timeout
   local name=$1 to=$2; shift 2
   timeout -k 10 $to "$@" > $OUT/$name.log 2>&1
   local rc=$?
-  echo "$name rc=$rc"; tail -3 $OUT/$name.log
+  echo "$name rc=$rc"; tail -2 $OUT/$name.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
-  return $rc
+  return 0
 }
 
-step pytest_gpu 900 python3 -m pytest tests -q -m gpu -rA
-step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python3 bench.py
-if [ "$2" != "--no-prof" ]; then
-  step prof_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu
-  step prof_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu
-  step prof_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu
-  step prof_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU --output-format csv -d $OUT/prof_sq -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu
+if [ "$2" != "--no-tests" ]; then
+  step pytest 420 python3 -u -m pytest tests -m gpu -rA -v --timeout 300 --timeout-method thread
+  step smoke 120 python3 -c "import __graft_entry__ as g; g.smoke()"
 fi
+step bench_C2 240 python3 bench.py
+for cfg in C1 C3 C4 C5; do
+  step bench_$cfg 240 python3 bench.py --config $cfg --no-cpu
+done
+PB="bench.py --steps 5 --warmup 1 --no-cpu --no-roof --interactive-frames 0"
+for cfg in C2 C3 C5; do
+  step trace_$cfg 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$cfg -o run -- python3 $PB --config $cfg
+  step fetch_$cfg 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch_$cfg -o run -- python3 $PB --config $cfg
+  step write_$cfg 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write_$cfg -o run -- python3 $PB --config $cfg
+done
 exit 0

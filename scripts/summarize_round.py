@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Summarise a scripts/gpu_r02.sh output directory into profiles/.
+"""Summarise a scripts/gpu_round.sh output directory into profiles/.
 
-  python scripts/summarize_r02.py gpurun_out/<tag> <round-name>
+  python scripts/summarize_round.py gpurun_out/<tag> <round-name>
 
 Per config with a trace_<cfg>/ fetch_<cfg>/ write_<cfg>/ triple (bench.py
 --steps 5 --warmup 1 under rocprofv3):
@@ -85,7 +85,7 @@ def main():
     src, name = sys.argv[1], sys.argv[2]
     prof = os.path.join(REPO, "profiles")
     md = [f"# Profile {name}\n",
-          f"Source: `scripts/gpu_r02.sh` on one MI355X (`{os.path.basename(src.rstrip('/'))}`); "
+          f"Source: `scripts/gpu_round.sh` on one MI355X (`{os.path.basename(src.rstrip('/'))}`); "
           "rocprofv3 runs of `bench.py --steps 5 --warmup 1 --no-cpu --no-roof --interactive-frames 0 --config <C>`; "
           f"durations and counters averaged over the {STEPS} timed dispatches of each production kernel "
           "(warmup and the untimed counting kernels excluded).\n"]

@@ -79,7 +79,7 @@ def test_bench_two_ranks_gloo_rehearsal(native):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.update(VRHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--frames-per-step", "2", "--no-cpu", "--no-roof", "--interactive-frames", "2"]
+           "--frames-per-step", "2", "--no-cpu", "--no-roof", "--interactive-frames", "2", "--strong-steps", "2"]
     res = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
@@ -87,3 +87,12 @@ def test_bench_two_ranks_gloo_rehearsal(native):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["scaling"] == "strong"
     assert out["config"]["parallelism"] == "tile2" and out["interactive"]["frames_per_step"] == 1
+    # rays: reference-equivalent and traced, side by side (the camera ray is traced once per pixel per launch)
+    assert out["mrays_per_s"] > 0 and 0 < out["mrays_per_s_traced"] <= out["mrays_per_s"]
+    assert 0 < out["rays_per_path_traced"] <= out["rays_per_path"]
+    # the fixed-cadence view: 16 frames per step for this N, against a 1-GPU rate measured in the same run
+    st = out["strong"]
+    assert st["frames_per_step"] == 16 and st["value"] > 0 and st["one_gpu_value"] > 0
+    assert abs(st["efficiency"] - st["value"] / (2 * st["one_gpu_value"])) < 1e-3
+    # kernel time is the union of overlapping launch spans: never more than the step
+    assert out["roofline"]["avg_launch_ms"] <= out["ms_per_step"] * 1.001

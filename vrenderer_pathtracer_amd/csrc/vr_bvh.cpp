@@ -542,6 +542,7 @@ int validate_flat(const float* bvh, size_t n_bvh_f4, const float* verts, size_t 
     if (!bvh || n_bvh_f4 < 4 || (n_bvh_f4 % 4) != 0 || !verts || n_slots == 0) return -1;
     const size_t n_nodes = n_bvh_f4 / 4;
     std::vector<uint8_t> seen(n_nodes, 0);
+    std::vector<uint8_t> leaf_seen(n_slots, 0);                // a leaf run referenced twice: a DAG too
     std::vector<std::pair<size_t, uint32_t>> st{ { 0, 1 } };   // (node float4 offset, depth)
     uint32_t max_depth = 0, count = 0;
     while (!st.empty()) {
@@ -562,6 +563,12 @@ int validate_flat(const float* bvh, size_t n_bvh_f4, const float* verts, size_t 
                 st.push_back({ (size_t)idx, d + 1 });
             } else {
                 size_t s = (size_t)(~idx);
+                // every leaf has exactly one parent: the device layout's
+                // per-triangle root paths (the equal-t tie-break) need a tree
+                if (s < n_slots) {
+                    if (leaf_seen[s]) return -6;
+                    leaf_seen[s] = 1;
+                }
                 // leaf run: triples until the terminator
                 for (;;) {
                     if (s >= n_slots) return -5;

@@ -11,17 +11,27 @@
 // mode) reproduces them bit for bit.
 //
 // MI355X mapping:
-//   * one workgroup = one 16x16 pixel tile (the reference block, so grid
-//     truncation is identical), four wave64s each owning an 8x8 sub-tile;
-//   * the traversal stack lives in LDS, entry-major ([depth][256 lanes]) so
-//     a wave's push/pop is one conflict-free ds_write/ds_read_b32;
+//   * mesh scenes: a persistent path-pool kernel (render_wave_kernel) drains
+//     work queues of 64-path chunks; each lane runs one path at a time
+//     through a resumable state machine and takes the next path when its
+//     own ends (ballot + mbcnt refill), so divergent path lengths do not idle
+//     the SIMD;
+//   * sphere-only scenes: render_kernel, one workgroup per 16x16 pixel tile
+//     (the reference block, so grid truncation is identical), four wave64s
+//     each owning an 8x8 sub-tile;
+//   * the traversal stack lives in LDS, entry-major ([depth][lanes]) so a
+//     wave's push/pop is one conflict-free ds_write/ds_read_b32, next to an
+//     LDS copy of the top of the (area-ordered) tree;
 //   * the while-while traversal switches to leaf processing on a wave64
 //     __ballot (the reference's 32-lane vote.ballot, :353-363);
 //   * leaf hits record only (t, slot, u, v); hit attributes are fetched once
 //     per ray after traversal (result-identical: only the final accepted hit
 //     is observable), cutting gathers on the hot loop;
-//   * all K frames of a render step run in one launch with the pixel's
-//     float4 accumulator kept in registers (one HBM read + one write per step).
+//   * all K frames of a render step run in one launch.  Paths store their
+//     radiance to a scratch buffer and finish_kernel adds each pixel's paths
+//     in path order (bit-identical to the reference's in-order sums); one-path-
+//     group sphere launches accumulate in registers instead (render_kernel,
+//     RenderParams::use_scratch = 0).
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 #include "vr_params.hpp"
@@ -120,31 +130,12 @@ struct Cnt {
     // instrumented production kernels (F_COUNT_EXEC) only
     // and its lane loads by width (16 / 12 / 8 / 4 B) at every global-load site
     uint32_t nodes_lds = 0, tri_loads = 0, mesh_hits = 0, nmap_hits = 0, ld128 = 0, ld96 = 0, ld64 = 0, ld32 = 0;
-#if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS)
-    // diagnostic builds only.  VR_TIMING: per-lane s_memtime cycles in
-    // spheres, mesh traversal, hit materialisation, shading, tonemap, whole
-    // kernel.  VR_LANESTATS: active lanes and wave iterations of the node
-    // loop, the triangle loop and the shading block (SIMD utilisation).
-    uint64_t tm[6] = { 0, 0, 0, 0, 0, 0 };
+#ifdef VR_PATH_TIMES
+    // diagnostic build: per-lane node visits, triangle tests and outer
+    // traversal iterations, recorded per path with its start and end time
+    uint32_t d_nodes = 0, d_tris = 0, d_iters = 0;
 #endif
 };
-#ifdef VR_LANESTATS
-#define VR_LANE(sl, si)                                                              \
-    do {                                                                             \
-        const unsigned long long m_ = __ballot(1);                                   \
-        cnt.tm[sl] += 1;                                                             \
-        if ((int)__lane_id() == __ffsll((long long)m_) - 1) cnt.tm[si] += 1;         \
-    } while (0)
-#else
-#define VR_LANE(sl, si) (void)0
-#endif
-#ifdef VR_TIMING
-#define VR_T0(name) const uint64_t name = __builtin_amdgcn_s_memtime()
-#define VR_T1(name, slot) cnt.tm[slot] += __builtin_amdgcn_s_memtime() - name
-#else
-#define VR_T0(name) (void)0
-#define VR_T1(name, slot) (void)0
-#endif
 
 // Counting launches (COUNT) come in two kinds: the reference algorithm's
 // event counts (no primary-hit reuse, no last-bounce shortcut)
@@ -209,24 +200,14 @@ constexpr int kLeafCountBits = 7;
 #define VR_LDS_BUDGET (40960 - 256)
 #endif
 constexpr int kLdsBudget = VR_LDS_BUDGET;
-#ifndef VR_STACK_CULL_MAX
-#define VR_STACK_CULL_MAX 0    // stack classes <= this carry entry distances (6 B per entry instead of 4);
-                               // off: measured C2 -13 %, C3 -8 % (16-entry class), and the
-                               // 24-entry stacks of C5 would not fit two 768-thread blocks per CU
-#endif
-constexpr bool stack_cull(int stack) { return stack <= VR_STACK_CULL_MAX; }
-constexpr int stack_entry_bytes(int stack) { return stack_cull(stack) ? 6 : 4; }
 constexpr int cache_nodes(int stack, int extra = 0, int bt = kBlockThreads) {
-    return ((bt / kBlockThreads) * kLdsBudget - stack * bt * stack_entry_bytes(stack) - extra) / 56 > 0 ?
-           ((bt / kBlockThreads) * kLdsBudget - stack * bt * stack_entry_bytes(stack) - extra) / 56 : 1;
+    return ((bt / kBlockThreads) * kLdsBudget - stack * bt * 4 - extra) / 56 > 0 ?
+           ((bt / kBlockThreads) * kLdsBudget - stack * bt * 4 - extra) / 56 : 1;
 }
 // Raw buffer loads for the node and triangle arrays: a 32-bit lane offset
 // against an SGPR descriptor (bounds-checked, no 64-bit address math), and an
-// explicit width per fetch (16 B node rows, 8 B child indices, 12 B vertices).
-// cache policy bits of the triangle loads (aux operand of the buffer loads)
-#ifndef VR_TRI_CPOL
-#define VR_TRI_CPOL 0
-#endif
+// explicit width per fetch (16 B node rows and triangle-pair rows, 8 B child
+// indices and pair tails).
 typedef unsigned int vr_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int vr_u32x3 __attribute__((ext_vector_type(3)));
 typedef unsigned int vr_u32x4 __attribute__((ext_vector_type(4)));
@@ -237,37 +218,22 @@ __device__ __forceinline__ vr4 buf_load4(__amdgpu_buffer_rsrc_t b, int off) {
     const vr_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, 0);
     return mk4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
-__device__ __forceinline__ vr3 buf_load3(__amdgpu_buffer_rsrc_t b, int off) {
-    const vr_u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(b, off, 0, VR_TRI_CPOL);
-    return vr3{ __uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z) };
-}
-__device__ __forceinline__ int4 buf_load4i(__amdgpu_buffer_rsrc_t b, int off) {
-    const vr_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, 0);
-    return make_int4((int)v.x, (int)v.y, (int)v.z, (int)v.w);
-}
 __device__ __forceinline__ int2 buf_load2i(__amdgpu_buffer_rsrc_t b, int off) {
     const vr_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(b, off, 0, 0);
     return make_int2((int)v.x, (int)v.y);
 }
 
-// Conservative fp16 node boxes for the culled traversal (default; -DVR_FP32_NODES
-// keeps the reference's fp32 rows): two 16-B loads per node visit instead of
-// four, the vector-memory instructions this kernel is bound by (C2 +9 %, C3
-// +5 %, C5 +5 % on the 6-wave kernel).  Rounded outward, a box only grows, so
-// no hit is lost; the looser boxes change the visit order, which the exact
-// equal-t tie-break (ref_first) makes irrelevant to the result: images equal
-// the fp32 and the strict traversal bit for bit (C5 differed in one pixel in
-// 8.3 M without it).
-#ifndef VR_FP32_NODES
-constexpr bool kFp16Nodes = true;
-#else
-constexpr bool kFp16Nodes = false;
-#endif
+// The t-culled traversal (default) reads conservative fp16 node boxes: two
+// 16-B loads per node visit instead of four, the vector-memory instructions
+// this kernel is bound by (C2 +9 %, C3 +5 %, C5 +5 % on the 6-wave kernel).
+// Rounded outward, a box only grows, so no hit is lost; the looser boxes
+// change the visit order, which the exact equal-t tie-break (ref_first) makes
+// irrelevant to the result: images equal the fp32 and the strict traversal
+// bit for bit (C5 differed in one pixel in 8.3 M without it).  The strict
+// traversal (F_STRICT) reads the reference's fp32 rows.
 
 struct Lds {
     int* stk;                 // this thread's column of the stack
-    unsigned short* stk16;    // F_LDS_TREE: 16-bit entries, (parent node << 1) | child slot; 0xffff = sentinel
-    unsigned short* tstk;     // entry distance of each stacked child (bf16, rounded down)
     const vr4* nodes;         // fp32 nodes: 3 rows per cached node; fp16 nodes: 2 rows per node
     const int2* idx;          // fp32 nodes: child indices per cached node
     int n_cached;             // nodes [0, n_cached) are read from LDS
@@ -283,27 +249,14 @@ struct Trav {
     float ivx, ivy, ivz, odx, ody, odz;
     float t, tcull, bu, bv;
     int best, sp, nodeAddr;
-    float tcur;               // slab entry of nodeAddr's box (a lower bound; 0 for the root)
-    int k, kend;              // leaf in progress (trav_step only)
 };
 
-// Stacked children carry their slab entry distance, rounded down to bf16
-// (the high half of a non-negative float's bits): a popped subtree or leaf
-// whose entry already lies beyond the closest hit (tcull) is skipped without
-// fetching it -- the same test that culls a child when it is first met, made
-// again with the closest hit found since.  Strict mode never culls.
-__device__ __forceinline__ unsigned short tkey(float t) { return (unsigned short)(__float_as_uint(t) >> 16); }
-__device__ __forceinline__ float tkey_f(unsigned short k) { return __uint_as_float((uint32_t)k << 16); }
-
-template <uint32_t FEAT, bool SC>
+template <uint32_t FEAT>
 __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, float t0, Trav& tr, const Lds& L)
 {
     tr.sp = 0;
-    if (HAS(F_LDS_TREE)) L.stk16[0] = 0xffffu;
-    else L.stk[0] = kSentinel;
-    if (SC) L.tstk[0] = 0;
+    L.stk[0] = kSentinel;
     tr.nodeAddr = 0;
-    tr.tcur = 0.f;
     // invDir (PathTracer.cu:289-294): components with |d| <= eps become +eps,
     // so |d| >= eps > 2^-32 and rcp_rn is the IEEE quotient unless a
     // component exceeds 2^125 (then the wave divides)
@@ -325,83 +278,43 @@ __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, f
     tr.tcull = HAS(F_STRICT) ? __builtin_inff() : t0 * 1.0009765625f;
     tr.best = -1;
     tr.bu = tr.bv = 0.f;
-    tr.k = tr.kend = 0;
 }
 
-// One outer iteration: the inner node loop until this lane holds a leaf and
-// the wave agrees (ballot), then the leaf loop.  Precondition: tr.nodeAddr is
-// an inner node (not kSentinel).
-// Pop (:339-342 and the leaf-loop pops), with the popped entry's distance in
-// tr.tcur.  sp reaches -1 only by popping the sentinel, after which nothing
-// is popped.
-template <bool SC>
+// Pop (:339-342 and the leaf-loop pops).  sp reaches -1 only by popping the
+// sentinel, after which nothing is popped.
 __device__ __forceinline__ int trav_pop(Trav& tr, const Lds& L)
 {
-    const int i = (tr.sp--) * L.stride;
-    tr.tcur = SC ? tkey_f(L.tstk[i]) : 0.f;
-    return L.stk[i];
-}
-
-// F_LDS_TREE: a stack entry names the pushed child by its parent and slot;
-// the child reference is read back from the parent's LDS row (ds_read_b32)
-__device__ __forceinline__ int lt_ref(const Lds& L, uint32_t e)
-{
-    if (e == 0xffffu) return kSentinel;
-    return __float_as_int(reinterpret_cast<const float*>(L.nodes + 2u * (e >> 1) + 1u)[2u + (e & 1u)]);
-}
-template <uint32_t FEAT, bool SC>
-__device__ __forceinline__ int trav_pop_f(const RenderParams& p, Trav& tr, const Lds& L)
-{
-    if (HAS(F_LDS_TREE)) {
-        const int i = (tr.sp--) * L.stride;
-        tr.tcur = 0.f;
-        return lt_ref(L, L.stk16[i]);
-    }
-    return trav_pop<SC>(tr, L);
+    return L.stk[(tr.sp--) * L.stride];
 }
 
 // One inner-node visit (:295-343): fetch (LDS copy or L2/HBM), two slab
 // tests, near child next, far child pushed when both are entered, pop when
 // neither is.  Leaves in tr.nodeAddr are left to the caller.
-template <bool COUNT, uint32_t FEAT, bool SC>
+template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
     int* stk = L.stk;
     const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
-    // a popped node whose box starts beyond the closest hit: not fetched,
-    // treated as entering neither child (pop the next)
-    const bool dead = SC && tr.tcur > tr.tcull;
-    if (COUNT) cnt.nodes += dead ? 0u : 1u;
-    VR_LANE(0, 1);
-    vr4 n0 = mk4(0.f, 0.f, 0.f, 0.f), n1 = n0, nz = n0;
-    int idx0 = 0, idx1 = 0;
+    if (COUNT) cnt.nodes += 1u;
+#ifdef VR_PATH_TIMES
+    cnt.d_nodes++;
+#endif
+    vr4 n0, n1, nz;
+    int idx0, idx1;
     const int node = tr.nodeAddr >> 2;
     // wave-uniform choice between the LDS copy and L2/HBM: a diverged wave
     // would pay both round trips
-#ifdef VR_NODE_STAMPS
-    uint64_t ns0;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns0) :: "memory");
-#endif
-#ifdef VR_LDS_PER_LANE
-    const bool in_lds = node < L.n_cached;                       // per lane: both paths may issue
-#else
-    const bool in_lds = __ballot(!dead && node >= L.n_cached) == 0ull;
-#endif
-    if (COUNT && !dead && HAS(F_LDS_TREE)) cnt.nodes_lds++;
-    else if (COUNT && !dead) {
+    const bool in_lds = __ballot(node >= L.n_cached) == 0ull;
+    if (COUNT) {
         cnt.nodes_lds += in_lds ? 1u : 0u;
-        if (!in_lds) { cnt.ld128 += (kFp16Nodes && !strict) ? 2u : 3u; cnt.ld64 += (kFp16Nodes && !strict) ? 0u : 1u; }
+        if (!in_lds) { cnt.ld128 += strict ? 3u : 2u; cnt.ld64 += strict ? 1u : 0u; }
     }
-    if (dead) {
-    } else if (kFp16Nodes && !strict) {
+    if (!strict) {
         // conservative fp16 boxes (lows rounded down, highs up): two 16-B
         // fetches per node instead of four; a box can only grow, so no hit
         // the exact box admits is lost
         vr4 a, b;
-        if (HAS(F_LDS_TREE)) {                          // the whole tree is in LDS: two ds_read_b128
-            a = L.nodes[2 * node];
-            b = L.nodes[2 * node + 1];
-        } else if (in_lds) {
+        if (in_lds) {
             a = L.nodes[2 * node];
             b = L.nodes[2 * node + 1];
         } else {
@@ -436,13 +349,6 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
         idx0 = ni.x;
         idx1 = ni.y;
     }
-#ifdef VR_NODE_STAMPS
-    uint64_t ns1;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns1) :: "memory");
-    asm volatile("" ::"v"(n0.x), "v"(n1.x), "v"(nz.x), "v"(idx0), "v"(idx1));
-    cnt.tm[0] += ns1 - ns0;
-    cnt.tm[2] += 1;
-#endif
     // slab distances n*inv - o*inv (:307-322); the culled mode lets
     // them contract to one v_fma each (more accurate)
     auto slab = [&](float n, float iv, float od) {
@@ -467,162 +373,18 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     // keep the child-index load in the same round trip as the bounds
     asm volatile("" ::"v"(idx0), "v"(idx1));
     const bool swp = (c1min < c0min);
-    const bool tc0 = !dead && (c0max >= c0min) && (c0min <= tr.tcull);
-    const bool tc1 = !dead && (c1max >= c1min) && (c1min <= tr.tcull);
+    const bool tc0 = (c0max >= c0min) && (c0min <= tr.tcull);
+    const bool tc1 = (c1max >= c1min) && (c1min <= tr.tcull);
     // branch-free push/pop: near child next, far child pushed when both
     // are hit, pop when neither is (same order as :324-343)
     const bool both = tc0 && tc1;
     const bool none = !tc0 && !tc1;
     const int nearc = (both && swp) ? idx1 : (tc0 ? idx0 : idx1);
     const int farc = swp ? idx0 : idx1;
-    const float near_t = (both && swp) ? c1min : (tc0 ? c0min : c1min);
-    const float far_t = swp ? c0min : c1min;
-#ifdef VR_NODE_STAMPS
-    {
-        uint64_t ns2;
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ns2) :: "memory");
-        cnt.tm[1] += ns2 - ns1;
-    }
-#endif
-    if (HAS(F_LDS_TREE)) {
-        const uint32_t etop = L.stk16[tr.sp * L.stride];
-        if (both) L.stk16[(tr.sp + 1) * L.stride] = (unsigned short)(((uint32_t)node << 1) | (swp ? 0u : 1u));
-        tr.sp += both ? 1 : (none ? -1 : 0);
-        tr.nodeAddr = none ? lt_ref(L, etop) : nearc;
-        tr.tcur = 0.f;
-        return;
-    }
     const int top = stk[tr.sp * L.stride];
-    const float ttop = SC ? tkey_f(L.tstk[tr.sp * L.stride]) : 0.f;
-    if (both) {
-        stk[(tr.sp + 1) * L.stride] = farc;
-        if (SC) L.tstk[(tr.sp + 1) * L.stride] = tkey(far_t);
-    }
+    if (both) stk[(tr.sp + 1) * L.stride] = farc;
     tr.sp += both ? 1 : (none ? -1 : 0);
     tr.nodeAddr = none ? top : nearc;
-    tr.tcur = SC ? (none ? ttop : near_t) : 0.f;
-}
-
-// One visit of a 4-wide node (F_WIDE, t-culled mode only): four slab tests
-// against the exact fp32 boxes of the collapsed binary tree, the entered
-// children ordered by entry distance, the nearest next and the others pushed
-// far to near.  Visits half as many nodes per ray as the binary walk; the
-// closest hit is the same (only the order among equal-distance hits can
-// differ, as for any culled order).
-template <bool COUNT, uint32_t FEAT, bool SC>
-__device__ __forceinline__ void node_step4(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
-{
-    int* stk = L.stk;
-    if (COUNT) cnt.nodes++;
-    VR_LANE(0, 1);
-    const __amdgpu_buffer_rsrc_t b4 = buf_rsrc(p.bvh4, p.n_nodes4 * 112u);
-    const int off = tr.nodeAddr * 16;
-    const vr4 lx = buf_load4(b4, off), hx = buf_load4(b4, off + 16);
-    const vr4 ly = buf_load4(b4, off + 32), hy = buf_load4(b4, off + 48);
-    const vr4 lz = buf_load4(b4, off + 64), hz = buf_load4(b4, off + 80);
-    const int4 ci = buf_load4i(b4, off + 96);
-    auto sl = [&](float n, float iv, float od) { return __builtin_fmaf(n, iv, -od); };
-    float key[4];
-    int val[4];
-    auto child = [&](int i, float lxi, float hxi, float lyi, float hyi, float lzi, float hzi, int idx) {
-        const float a0 = sl(lxi, tr.ivx, tr.odx), a1 = sl(hxi, tr.ivx, tr.odx);
-        const float b0 = sl(lyi, tr.ivy, tr.ody), b1 = sl(hyi, tr.ivy, tr.ody);
-        const float c0 = sl(lzi, tr.ivz, tr.odz), c1 = sl(hzi, tr.ivz, tr.odz);
-        const float tmin = span_begin(a0, a1, b0, b1, c0, c1, 0.0f);
-        const float tmax = span_end(a0, a1, b0, b1, c0, c1, 1e20f);
-        const bool hit = (tmax >= tmin) && (tmin <= tr.tcull) && (idx != kSentinel);
-        key[i] = hit ? tmin : __builtin_inff();
-        val[i] = idx;
-    };
-    child(0, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, ci.x);
-    child(1, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, ci.y);
-    child(2, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, ci.z);
-    child(3, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, ci.w);
-    const int n = (key[0] != __builtin_inff()) + (key[1] != __builtin_inff()) + (key[2] != __builtin_inff()) +
-                  (key[3] != __builtin_inff());
-    auto cs = [&](int i, int j) {                          // compare-swap, ties keep slot order
-        const bool sw = key[j] < key[i];
-        const float ki = key[i], kj = key[j];
-        const int vi = val[i], vj = val[j];
-        key[i] = sw ? kj : ki; key[j] = sw ? ki : kj;
-        val[i] = sw ? vj : vi; val[j] = sw ? vi : vj;
-    };
-    cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
-    const int top = stk[tr.sp * L.stride];
-    const float ttop = SC ? tkey_f(L.tstk[tr.sp * L.stride]) : 0.f;
-    if (n >= 4) { stk[(tr.sp + 1) * L.stride] = val[3]; if (SC) L.tstk[(tr.sp + 1) * L.stride] = tkey(key[3]); }
-    tr.sp += n >= 4 ? 1 : 0;
-    if (n >= 3) { stk[(tr.sp + 1) * L.stride] = val[2]; if (SC) L.tstk[(tr.sp + 1) * L.stride] = tkey(key[2]); }
-    tr.sp += n >= 3 ? 1 : 0;
-    if (n >= 2) { stk[(tr.sp + 1) * L.stride] = val[1]; if (SC) L.tstk[(tr.sp + 1) * L.stride] = tkey(key[1]); }
-    tr.sp += n >= 2 ? 1 : (n == 0 ? -1 : 0);
-    tr.nodeAddr = n == 0 ? top : val[0];
-    tr.tcur = SC ? (n == 0 ? ttop : key[0]) : 0.f;
-}
-
-// One visit of a quantized 4-wide node (F_Q4): three 16-B loads, the four
-// child boxes decoded as origin + q * 2^e per axis (one byte-to-float convert
-// and one FMA per bound, the slab distance directly: q * (s / d) + (origin -
-// o) / d), the entered children ordered by entry distance, the nearest next
-// and the others pushed far to near (at most 3 per level: the kQ4Stack class).
-template <bool COUNT, uint32_t FEAT, bool SC>
-__device__ __forceinline__ void node_stepQ4(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
-{
-    int* stk = L.stk;
-    if (COUNT) { cnt.nodes++; cnt.ld128 += 3; }
-    VR_LANE(0, 1);
-    const __amdgpu_buffer_rsrc_t qb = buf_rsrc(p.bvhq, p.n_nodesq * 48u);
-    const int off = tr.nodeAddr * 48;
-    const vr_u32x4 w0 = __builtin_amdgcn_raw_buffer_load_b128(qb, off, 0, 0);
-    const vr_u32x4 w1 = __builtin_amdgcn_raw_buffer_load_b128(qb, off + 16, 0, 0);
-    const vr_u32x4 w2 = __builtin_amdgcn_raw_buffer_load_b128(qb, off + 32, 0, 0);
-    auto h2f = [](uint32_t h) { return __half2float(__ushort_as_half((unsigned short)(h & 0xffffu))); };
-    const float ox = h2f(w0.x), oy = h2f(w0.x >> 16), oz = h2f(w0.y);
-    const float sx = __uint_as_float((((w0.y >> 16) & 31u) + p.q4_ebias) << 23);
-    const float sy = __uint_as_float((((w0.y >> 21) & 31u) + p.q4_ebias) << 23);
-    const float sz = __uint_as_float((((w0.y >> 26) & 31u) + p.q4_ebias) << 23);
-    const float ax = sx * tr.ivx, ay = sy * tr.ivy, az = sz * tr.ivz;   // exact: powers of two
-    const float bx = __builtin_fmaf(ox, tr.ivx, -tr.odx);
-    const float by = __builtin_fmaf(oy, tr.ivy, -tr.ody);
-    const float bz = __builtin_fmaf(oz, tr.ivz, -tr.odz);
-    float key[4];
-    int val[4];
-    auto child = [&](int i, int idx) {
-        const uint32_t sh = 8u * (uint32_t)i;
-        auto q = [&](uint32_t w) { return (float)((w >> sh) & 0xffu); };   // v_cvt_f32_ubyteN
-        const float a0 = __builtin_fmaf(q(w0.z), ax, bx), a1 = __builtin_fmaf(q(w0.w), ax, bx);
-        const float b0 = __builtin_fmaf(q(w1.x), ay, by), b1 = __builtin_fmaf(q(w1.y), ay, by);
-        const float c0 = __builtin_fmaf(q(w1.z), az, bz), c1 = __builtin_fmaf(q(w1.w), az, bz);
-        const float tmin = span_begin(a0, a1, b0, b1, c0, c1, 0.0f);
-        const float tmax = span_end(a0, a1, b0, b1, c0, c1, 1e20f);
-        const bool hit = (tmax >= tmin) && (tmin <= tr.tcull) && (idx != kSentinel);
-        key[i] = hit ? tmin : __builtin_inff();
-        val[i] = idx;
-    };
-    child(0, (int)w2.x);
-    child(1, (int)w2.y);
-    child(2, (int)w2.z);
-    child(3, (int)w2.w);
-    const int n = (key[0] != __builtin_inff()) + (key[1] != __builtin_inff()) + (key[2] != __builtin_inff()) +
-                  (key[3] != __builtin_inff());
-    auto cs = [&](int i, int j) {                          // compare-swap, ties keep slot order
-        const bool sw = key[j] < key[i];
-        const float ki = key[i], kj = key[j];
-        const int vi = val[i], vj = val[j];
-        key[i] = sw ? kj : ki; key[j] = sw ? ki : kj;
-        val[i] = sw ? vj : vi; val[j] = sw ? vi : vj;
-    };
-    cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
-    const int top = stk[tr.sp * L.stride];
-    if (n >= 4) stk[(tr.sp + 1) * L.stride] = val[3];
-    tr.sp += n >= 4 ? 1 : 0;
-    if (n >= 3) stk[(tr.sp + 1) * L.stride] = val[2];
-    tr.sp += n >= 3 ? 1 : 0;
-    if (n >= 2) stk[(tr.sp + 1) * L.stride] = val[1];
-    tr.sp += n >= 2 ? 1 : (n == 0 ? -1 : 0);
-    tr.nodeAddr = n == 0 ? top : val[0];
-    tr.tcur = 0.f;
-    (void)SC;
 }
 
 // Equal-t tie-break of the culled traversal.  The reference keeps the first
@@ -668,22 +430,20 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 {
     const bool strict = HAS(F_STRICT);
     if (COUNT) cnt.tris++;
-    VR_LANE(2, 3);
+#ifdef VR_PATH_TIMES
+    cnt.d_tris++;
+#endif
     const vr4 v0 = mk4(t.a0.x, t.a0.y, t.a0.z, 0.f);
     const vr4 e1 = mk4(t.a1.x, t.a1.y, t.a1.z, 0.f);         // v1 - v0, v2 - v0 (RayIntersection.cuh:62-63), from the upload
     const vr4 e2 = mk4(t.a2.x, t.a2.y, t.a2.z, 0.f);
     const vr4 pv = cross4(r.d, e2);
     const float det = dot4(e1, pv);
-#ifndef VR_IEEE_DIV
     // 1/det (RayIntersection.cuh:75): only lanes with |det| >= VR_EPS (> 2^-32) can accept the
     // hit, and there rcp_rn is the IEEE quotient up to |det| = 2^125; a wave
     // holding a larger (or non-finite) det takes the division
     float inv_det;
     if (__builtin_expect(__ballot(!(__builtin_fabsf(det) <= kRcpRnHi)) != 0ull, 0)) inv_det = 1.f / det;
     else inv_det = rcp_rn(det);
-#else
-    const float inv_det = 1.f / det;
-#endif
     const vr4 tv = sub4(r.o, v0);
     const float u = dot4(tv, pv) * inv_det;
     const vr4 q = cross4(tv, e1);
@@ -695,47 +455,18 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
         tr.t = dist; tr.best = 3 * k; tr.bu = u; tr.bv = v;
         tr.tcull = strict ? tr.tcull : tr.t * 1.0009765625f;
     }
-#ifndef VR_NO_TIE_ORDER
     // a tie with the mesh's closest hit so far: keep the reference's first
     // (the strict walk tests in the reference order already)
     const bool tie = !strict && ok && dist > VR_EPS && dist == tr.t && tr.best >= 0 && 3 * k != tr.best;
     if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
         if (tie && ref_first(p, tr, k, tr.best / 3)) { tr.best = 3 * k; tr.bu = u; tr.bv = v; }
     }
-#endif
-}
-
-__device__ __forceinline__ TriV tri_load(const RenderParams& p, int k)
-{
-#ifdef VR_DROP_TRIS
-    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, 0u);     // timing probe: loads return 0
-#else
-    const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, p.n_tris * 36u);
-#endif
-    const int toff = k * 36;
-    TriV t;
-    t.a0 = buf_load3(tbuf, toff); t.a1 = buf_load3(tbuf, toff + 12); t.a2 = buf_load3(tbuf, toff + 24);
-    return t;
-}
-
-template <bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ void tri_test(const RenderParams& p, const Ray& r, Trav& tr, int k, Cnt& cnt)
-{
-    const TriV t = tri_load(p, k);
-    if (COUNT) { cnt.tri_loads++; cnt.ld96 += 3; }
-    asm volatile("" ::"v"(t.a0.x), "v"(t.a1.x), "v"(t.a2.x));   // three dwordx3 loads, one trip
-    tri_test_v<COUNT, FEAT>(p, r, tr, k, t, cnt);
 }
 
 // One outer iteration of the while-while loop: the inner node loop until
 // this lane holds a leaf and the wave agrees (ballot, :353-363), with one
 // leaf postponed (:345-351), then the leaf loop.  Precondition: tr.nodeAddr
 // is an inner node (not kSentinel).
-// Paired triangle loads as 4 x 16 B + 8 B over the pair's 72 contiguous bytes
-// (5 vector loads instead of 6: C2 +1 %, C3 +1 %, C5 +3 %); -DVR_TRI_B96 keeps 3 x 12 B per triangle.
-#ifndef VR_TRI_B96
-#define VR_TRI_B128
-#endif
 #ifndef VR_NODE_BREAK
 #define VR_NODE_BREAK 6    // measured (path kernel with paired triangle loads): 0 (the reference's
                            // all-lanes vote) C2 2,294, 2: 2,503, 4: 2,563, 6: 2,577, 8: 2,583 (C3 -2 %)
@@ -755,17 +486,15 @@ constexpr int node_break() {
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
-    constexpr bool SC = stack_cull(STACK);
+#ifdef VR_PATH_TIMES
+    cnt.d_iters++;
+#endif
     int leafAddr = 0;
-    float leafT = 0.f;                                          // slab entry of the postponed leaf
     while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
-        if (HAS(F_Q4)) node_stepQ4<COUNT, FEAT, SC>(p, r, tr, L, cnt);
-        else if (HAS(F_WIDE)) node_step4<COUNT, FEAT, SC>(p, r, tr, L, cnt);
-        else node_step<COUNT, FEAT, SC>(p, r, tr, L, cnt);
+        node_step<COUNT, FEAT>(p, r, tr, L, cnt);
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
             leafAddr = tr.nodeAddr;
-            leafT = tr.tcur;
-            tr.nodeAddr = trav_pop_f<FEAT, SC>(p, tr, L);
+            tr.nodeAddr = trav_pop(tr, L);
         }
         // the wave moves on to the leaves once (nearly) every lane holds one;
         // lanes still searching resume in the next outer iteration
@@ -773,17 +502,14 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
     }
     while (leafAddr < 0) {
         const int lv = ~leafAddr;
-        // a leaf whose box starts beyond the closest hit found since it was
-        // met holds no closer triangle: skipped
-        const int kend = (lv >> kLeafCountBits) + ((SC && leafT > tr.tcull) ? 0 : (lv & ((1 << kLeafCountBits) - 1)));
-#ifndef VR_NO_TRI_PAIRS
+        const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
         // the loads of two triangles in one trip (the tests stay in slot order):
-        // a leaf's triangles need half the dependent round trips (C2 +1 %, C3 +4 %)
+        // a leaf's triangles need half the dependent round trips (C2 +1 %, C3 +4 %),
+        // the pair's 72 contiguous bytes as 4 x 16 B + 8 B (5 loads instead of 6:
+        // C2 +1 %, C3 +1 %, C5 +3 %); past the array end the buffer descriptor
+        // returns zeros (never tested)
         for (int k = lv >> kLeafCountBits; k < kend; k += 2) {
             const bool two = k + 1 < kend;
-#ifdef VR_TRI_B128
-            // the pair's 72 contiguous bytes as 4 x 16 B + 8 B (5 loads instead of 6);
-            // past the array end the buffer descriptor returns zeros (never tested)
             TriV ta, tb;
             {
                 const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, p.n_tris * 36u);
@@ -795,48 +521,16 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
                 tb.a0 = vr3{ q2.y, q2.z, q2.w }; tb.a1 = vr3{ q3.x, q3.y, q3.z };
                 tb.a2 = vr3{ q3.w, __int_as_float(q4.x), __int_as_float(q4.y) };
             }
-#else
-            const TriV ta = tri_load(p, k), tb = tri_load(p, two ? k + 1 : k);
-#endif
             if (COUNT) {                                        // an odd leaf's last pair loads its triangle twice
                 cnt.tri_loads += 2;
-#ifdef VR_TRI_B128
                 cnt.ld128 += 4; cnt.ld64 += 1;
-#else
-                cnt.ld96 += 6;
-#endif
             }
             asm volatile("" ::"v"(ta.a0.x), "v"(ta.a1.x), "v"(ta.a2.x), "v"(tb.a0.x), "v"(tb.a1.x), "v"(tb.a2.x));
             tri_test_v<COUNT, FEAT>(p, r, tr, k, ta, cnt);
             if (two) tri_test_v<COUNT, FEAT>(p, r, tr, k + 1, tb, cnt);
         }
-#else
-        for (int k = lv >> kLeafCountBits; k < kend; ++k) tri_test<COUNT, FEAT>(p, r, tr, k, cnt);
-#endif
         leafAddr = tr.nodeAddr;
-        leafT = tr.tcur;
-        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop_f<FEAT, SC>(p, tr, L);
-    }
-}
-
-// If-if alternative: one unit of work per call -- the next triangle of the
-// leaf in progress, else one node visit; a leaf reached is started at once
-// (the leaves, and the triangles within each, are tested in the same order
-// as by trav_iter).  Lanes stay busy with whichever kind of step they need.
-template <bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ void trav_step(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
-{
-    if (tr.k < tr.kend) {
-        tri_test<COUNT, FEAT>(p, r, tr, tr.k, cnt);
-        ++tr.k;
-    } else {
-        node_step<COUNT, FEAT, false>(p, r, tr, L, cnt);
-    }
-    if (tr.k >= tr.kend && tr.nodeAddr < 0) {                // start the leaf, resume at the stack top
-        const int lv = ~tr.nodeAddr;
-        tr.k = lv >> kLeafCountBits;
-        tr.kend = tr.k + (lv & ((1 << kLeafCountBits) - 1));
-        tr.nodeAddr = trav_pop<false>(tr, L);
+        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop(tr, L);
     }
 }
 
@@ -849,11 +543,10 @@ template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
 {
     Trav tr;
-    trav_init<FEAT, stack_cull(STACK)>(p, r, hr.t, tr, L);
+    trav_init<FEAT>(p, r, hr.t, tr, L);
     while (tr.nodeAddr != kSentinel) trav_iter<STACK, COUNT, FEAT>(p, r, tr, L, cnt);
     trav_finish(tr, hr);
 }
-
 // intersectScene (PathTracer.cu:136-468): closest hit, attributes deferred.
 // intersectScene (PathTracer.cu:136-468), sphere part: Cornell walls and
 // light, the two small spheres, the example sphere.  Returns true when the
@@ -895,13 +588,9 @@ __device__ __forceinline__ bool intersect_spheres(const RenderParams& p, const R
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
 {
-    VR_T0(t_sph);
     const bool mesh = intersect_spheres<COUNT, FEAT>(p, r, hr, cnt);
-    VR_T1(t_sph, 0);
     if (mesh) {
-        VR_T0(t_mesh);
         traverse_mesh<STACK, COUNT, FEAT>(p, r, hr, L, cnt);
-        VR_T1(t_mesh, 1);
     }
     return hr.t < 1e20f;
 }
@@ -1118,9 +807,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         return true;
     }
     Hit h;
-    VR_T0(t_fill);
     fill_hit<FEAT>(p, ray, hr, h);
-    VR_T1(t_fill, 2);
     if (COUNT) {
         if (hr.kind == HK_MESH) {
             cnt.attr += 24 + 48;
@@ -1155,8 +842,6 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
     ps.accum = add4(ps.accum, mul4(ps.mask, h.em));
     ray.o = h.hp;
     const vr4 normal = h.n;
-    VR_T0(t_shade);
-    VR_LANE(4, 5);
     if (h.type == 0) {                                                   // :671-676
         ray.d = sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d)));
         ray.o = add4(ray.o, mul4s(normal, 0.05f));
@@ -1177,12 +862,6 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         } else {
             float rand1 = 2.f * VR_PI * ps.rng.uniform();
             float rand2 = ps.rng.uniform();
-#ifdef VR_PROBE_COHERENT
-            // probe only (invalid images): every lane shading in this step
-            // takes the first lane's direction sample -- the coherence bound
-            rand1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rand1)));
-            rand2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rand2)));
-#endif
             const float rand2s = sqrt_exact(rand2);
             const vr4 u = normalize4(cross4(axis, w));
             const vr4 v = cross4(w, u);
@@ -1201,10 +880,6 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
         float rand1 = 2.f * VR_PI * ps.rng.uniform();
         float rand2 = ps.rng.uniform();
-#ifdef VR_PROBE_COHERENT
-        rand1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rand1)));
-        rand2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rand2)));
-#endif
         const float rand2s = sqrt_exact(rand2);
         const vr4 u = normalize4(cross4(axis, w));
         const vr4 v = cross4(w, u);
@@ -1227,7 +902,6 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         ray.o = add4(ray.o, mul4s(normal, 0.05f));
         ray.d = newdir;
     }
-    VR_T1(t_shade, 3);
     if (++ps.bounce == 4) {
         ps.accum.w = ps.depth;
         out = ps.accum;
@@ -1323,20 +997,17 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
 // Binds this thread's stack column and fills the block's node cache with
 // the first nodes of the area-ordered node array.
 template <uint32_t FEAT, int BT = kBlockThreads>
-__device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, unsigned short* lds_tstk,
-                                         vr4* lds_nodes, int2* lds_idx,
+__device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, vr4* lds_nodes, int2* lds_idx,
                                          int cn, int tid)
 {
     Lds L;
     L.stk = lds_stack + tid;
-    L.tstk = lds_tstk + tid;
     L.stride = BT;
     L.nodes = lds_nodes;
     L.idx = lds_idx;
     L.n_cached = 0;
-#ifndef VR_NO_NODE_CACHE
-    if (HAS(F_MESH) && !HAS(F_WIDE)) {
-        if (kFp16Nodes && !HAS(F_STRICT)) {            // fp16 nodes, 32 B: 1.5x as many fit
+    if (HAS(F_MESH)) {
+        if (!HAS(F_STRICT)) {            // fp16 nodes, 32 B: 1.5x as many fit
             const uint32_t cap = (uint32_t)(3 * cn / 2);
             L.n_cached = (int)(p.n_nodes < cap ? p.n_nodes : cap);
             for (int i = tid; i < 2 * L.n_cached; i += BT) lds_nodes[i] = p.bvh16[i];
@@ -1348,7 +1019,6 @@ __device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, 
         }
         __syncthreads();
     }
-#endif
     return L;
 }
 
@@ -1376,11 +1046,10 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
 {
     constexpr int CN = cache_nodes(STACK);
     __shared__ int lds_stack[STACK * kBlockThreads];
-    __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * kBlockThreads : 1];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
     const int tid = threadIdx.x;
-    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, tid);
+    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
     // block -> (tile, path group): the 2*n_frames paths of a pixel are split
     // into p.split contiguous groups run by different blocks (strong-scaling
     // and tail balance); group g of tile t is block t*split + g
@@ -1395,7 +1064,6 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
     const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     if (x >= p.wr || y >= p.hr) return;   // never true for a valid launch
     Cnt cnt;
-    VR_T0(t_kernel);
 
     const uint32_t ind = x + y * p.W;
     const Ray cam = camera_ray(p, x, y);
@@ -1430,7 +1098,6 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
         last_w = result.w;
     }
     if (direct) {   // else finish_kernel accumulates the paths' results in path order
-        VR_T0(t_tone);
         // only the launch's last frame is observable in the colour and depth
         // surfaces (each frame of the reference overwrites them, :846-866)
         const unsigned char db = f2u8((1.f - last_w) * 255);
@@ -1438,20 +1105,7 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
         p.depth[ind] = dv;
         p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
         p.accum[ind] = io;
-        VR_T1(t_tone, 4);
     }
-#if defined(VR_TIMING) || defined(VR_LANESTATS)
-    VR_T1(t_kernel, 5);
-    if (p.counters) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            unsigned long long x = cnt.tm[k];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
-            if (lane == 0) atomicAdd(p.counters + 8 + k, x);
-        }
-    }
-#endif
     if (COUNT) flush_counts(p, cnt, lane, (FEAT & F_COUNT_EXEC) != 0u);
 }
 
@@ -1470,11 +1124,9 @@ template <int STACK, uint32_t FEAT>
 __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderParams p)
 {
     __shared__ int lds_stack[STACK * kBlockThreads];
-    __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * kBlockThreads : 1];
     const int tid = threadIdx.x;
     Lds L;
     L.stk = lds_stack + tid;
-    L.tstk = lds_tstk + tid;
     L.stride = kBlockThreads;
     L.nodes = nullptr;
     L.idx = nullptr;
@@ -1564,23 +1216,23 @@ static_assert((4 * VR_PATH_WAVES_CORNELL * 64) % VR_PATH_BLOCK_CORNELL == 0, "wh
 // c: the kernel is a Cornell-box specialisation (cornell_kernel<FEAT>())
 constexpr bool cornell_res(int stack, bool c) { return c && stack <= 16; }
 constexpr int wave_block(int stack, bool c) {
-    return cornell_res(stack, c) ? VR_PATH_BLOCK_CORNELL : stack <= kQ4Stack ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads;
+    return cornell_res(stack, c) ? VR_PATH_BLOCK_CORNELL : stack <= 24 ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads;
 }
 // Launches of fewer than 2^24 paths (sharded frames, RenderParams::small_blocks)
 // take 256-thread blocks at the same residency: a block frees its CU slot once
 // its 4 waves are done rather than 12, so the launch's drain overlaps the next
 // launch sooner.  Projected 8-rank C2 step 1.283 -> 1.193 ms (C3 0.468 ->
 // 0.420 ms), while whole frames keep the 768-thread blocks (C2 3,437 vs 3,244).
-constexpr int wave_block_small(int stack, bool c) { return stack <= kQ4Stack ? kBlockThreads : wave_block(stack, c); }
+constexpr int wave_block_small(int stack, bool c) { return stack <= 24 ? kBlockThreads : wave_block(stack, c); }
 constexpr int path_waves(int stack, bool c) {
-    return cornell_res(stack, c) ? VR_PATH_WAVES_CORNELL : stack <= kQ4Stack ? VR_PATH_WAVES : stack <= 32 ? 4 : 2;
+    return cornell_res(stack, c) ? VR_PATH_WAVES_CORNELL : stack <= 24 ? VR_PATH_WAVES : stack <= 32 ? 4 : 2;
 }
 constexpr int path_blocks_per_cu(int stack, int bt, bool c) { return 4 * path_waves(stack, c) * 64 / bt; }
 // LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
 // the node cache takes what the stacks leave (56 B per node)
 constexpr int path_cache_nodes(int stack, int bt, bool c) {
-    return (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * stack_entry_bytes(stack)) / 56 > 0
-               ? (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * stack_entry_bytes(stack)) / 56 : 1;
+    return (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * 4) / 56 > 0
+               ? (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * 4) / 56 : 1;
 }
 template <uint32_t FEAT>
 constexpr bool cornell_kernel() {
@@ -1613,35 +1265,10 @@ __global__ void __launch_bounds__(BT, path_waves(STACK, cornell_kernel<FEAT>()))
 {
     constexpr int CN = path_cache_nodes(STACK, BT, cornell_kernel<FEAT>());
     __shared__ int lds_stack[STACK * BT];
-    __shared__ unsigned short lds_tstk[stack_cull(STACK) ? STACK * BT : 1];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
-    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_tstk, lds_nodes, lds_idx, CN, (int)threadIdx.x);
+    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_nodes, lds_idx, CN, (int)threadIdx.x);
     wave_body<STACK, FEAT, BT>(p, L);
-}
-
-// F_LDS_TREE: the same path kernel with the whole conservative-fp16 tree
-// copied into each block's LDS (dynamic, 32 B per node) and 16-bit stack
-// entries, one 1,024-thread block per CU (4 waves per SIMD): every node visit
-// is two ds_read_b128 instead of two vector-memory loads, which is what the
-// texture path spends most of its time on (profiles/r02_c2_mem.md).
-template <uint32_t FEAT>
-__global__ void __launch_bounds__(kLdsTreeBlock, 4) render_wave_kernel_lt(const RenderParams p)
-{
-    __shared__ unsigned short lds_stk16[kLdsTreeStack * kLdsTreeBlock];
-    extern __shared__ vr4 lds_tree[];
-    const int tid = (int)threadIdx.x;
-    for (uint32_t i = (uint32_t)tid; i < 2u * p.n_nodes; i += (uint32_t)kLdsTreeBlock) lds_tree[i] = p.bvh16[i];
-    __syncthreads();
-    Lds L;
-    L.stk = nullptr;
-    L.stk16 = lds_stk16 + tid;
-    L.tstk = nullptr;
-    L.stride = kLdsTreeBlock;
-    L.nodes = lds_tree;
-    L.idx = nullptr;
-    L.n_cached = (int)p.n_nodes;
-    wave_body<kLdsTreeStack, FEAT, kLdsTreeBlock>(p, L);
 }
 
 template <int STACK, uint32_t FEAT, int BT>
@@ -1711,7 +1338,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     uint32_t cam_xy = 0;                                   // F_INLINE_PRIM: its pixel (x << 16 | y) until LS_CAMERA
 #ifdef VR_PATH_TIMES
     uint64_t pstart = 0;                                   // diagnostic: this lane's path start, primary hit kind
-    uint32_t pkind = 0;
+    uint32_t pkind = 0, p0n = 0, p0t = 0, p0i = 0;        // and its counts at the start
 #endif
     Ray ray;
     PathState ps;
@@ -1719,17 +1346,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     Trav tr;
     auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
         if (sub == ~0u) { state = LS_DONE; return; }
-#ifdef VR_PIXEL_MAJOR
-        // the sub-tile's items pixel-major: a chunk holds all paths of
-        // 64 / n_paths pixels, so a wave's bounce rays share their origins
-        {
-            const uint32_t e = path * 64u + px;
-            q = e % n_paths;
-            px = e / n_paths;
-        }
-#else
         q = path;
-#endif
         slot = sub * 64u + px;
         const uint32_t f = q >> 1;
         uint32_t x, y;
@@ -1741,6 +1358,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #ifdef VR_PATH_TIMES
         pstart = __builtin_amdgcn_s_memrealtime();
         pkind = 15u;
+        p0n = cnt.d_nodes; p0t = cnt.d_tris; p0i = cnt.d_iters;
 #endif
         if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {      // few paths per pixel: trace the camera ray here
             cam_xy = (x << 16) | y;                        // (set up at the top of the loop, out of the refill)
@@ -1766,9 +1384,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     };
     start(cur_sub, cur_q, (uint32_t)lane);
 
-    VR_T0(t_kernel);
     for (;;) {
-        VR_T0(t_setup);
         if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {
             if (state == LS_CAMERA) {
                 ray = camera_ray(p, cam_xy >> 16, cam_xy & 0xffffu);
@@ -1777,53 +1393,49 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         }
         if (state == LS_SETUP) {
             if (intersect_spheres<CNT, FEAT>(p, ray, hr, cnt)) {
-                trav_init<FEAT, stack_cull(STACK)>(p, ray, hr.t, tr, L);
+                trav_init<FEAT>(p, ray, hr.t, tr, L);
                 state = LS_TRAV;
             } else {
                 state = LS_SHADE;
             }
         }
-        VR_T1(t_setup, 0);
-        VR_T0(t_trav);
         if (HAS(F_MESH)) {
             for (;;) {
                 const int n_trav = __popcll(__ballot(state == LS_TRAV));
                 if (n_trav == 0) break;
                 const int n_shade = __popcll(__ballot(state == LS_SHADE));
                 if (n_shade >= VR_SHADE_BATCH && n_shade * VR_SHADE_RATIO >= n_trav) break;
-#ifndef VR_NO_DRAIN_EAGER
                 // queue drained: no lane will be refilled, so a path waiting to
                 // be shaded is only delayed by the others' traversal
                 if (cur_sub == ~0u && n_shade > 0) break;
-#endif
                 if (state == LS_TRAV) {
-#ifdef VR_IFIF
-                    trav_step<CNT, FEAT>(p, ray, tr, L, cnt);
-                    if (tr.nodeAddr == kSentinel && tr.k >= tr.kend) {
-#else
                     trav_iter<STACK, CNT, FEAT>(p, ray, tr, L, cnt);
                     if (tr.nodeAddr == kSentinel) {
-#endif
                         trav_finish(tr, hr);
                         state = LS_SHADE;
                     }
                 }
             }
         }
-        VR_T1(t_trav, 1);
-        VR_T0(t_shblk);
         bool ended = false;
         if (state == LS_SHADE) {
-            VR_LANE(4, 5);
             vr4 out;
+#ifdef VR_PATH_TIMES
+            if (ps.bounce == 0) pkind = (uint32_t)hr.kind;
+#endif
             if (bounce_step<CNT, FEAT>(p, ray, hr, ps, out, cnt)) {
                 store_path(p, q, slot, out, ps.depth);
 #ifdef VR_PATH_TIMES
                 const size_t pidx = (size_t)q * p.path_stride + slot;
-                if (p.counters && pidx < kPathTimesCap) {   // diagnostic: start, end | primary hit kind << 56 per path
-                    unsigned long long* pr = p.counters + kWaveTimesBase + 3 * 8192 + 2 * pidx;
+                if (p.counters && pidx < kPathTimesCap) {
+                    // diagnostic: start, end | primary hit kind << 56, and the
+                    // path's node visits | triangle tests << 20 | outer
+                    // traversal iterations << 40 (20 bits each)
+                    unsigned long long* pr = p.counters + kWaveTimesBase + 3 * 8192 + 3 * pidx;
                     pr[0] = pstart;
                     pr[1] = __builtin_amdgcn_s_memrealtime() | ((unsigned long long)pkind << 56);
+                    auto c20 = [](uint32_t v) { return (unsigned long long)(v < 0xfffffu ? v : 0xfffffu); };
+                    pr[2] = c20(cnt.d_nodes - p0n) | (c20(cnt.d_tris - p0t) << 20) | (c20(cnt.d_iters - p0i) << 40);
                 }
 #endif
                 ended = true;
@@ -1831,7 +1443,6 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 state = LS_SETUP;
             }
         }
-        VR_T1(t_shblk, 4);
         const unsigned long long em = __ballot(ended);
         if (em != 0ull) {
             const uint32_t need = (uint32_t)__popcll(em);
@@ -1858,18 +1469,6 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     }
 #endif
     if (CNT) flush_counts(p, cnt, lane, true);
-    VR_T1(t_kernel, 5);
-#if defined(VR_LANESTATS) || defined(VR_TIMING) || defined(VR_NODE_STAMPS)
-    if (p.counters) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            unsigned long long v = cnt.tm[k];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-            if (lane == 0) atomicAdd(p.counters + 8 + k, v);
-        }
-    }
-#endif
 }
 
 __global__ void half_to_float_kernel(const uint16_t* __restrict__ src, vr4* __restrict__ dst, size_t n)
@@ -1921,20 +1520,8 @@ __global__ void selftest_math_kernel(int fn, const float* a, const float* b, flo
 // ---- host launchers --------------------------------------------------------
 // Feature specialisations, smallest first (BASELINE configs C1..C5); the
 // generic kernel covers everything else, deep trees and the counting variant.
-// the 4-wide traversal is compiled in only with -DVR_BVH4 (the host sets the
-// runtime flag only then; such launches take the generic kernel)
-#ifdef VR_BVH4
-constexpr uint32_t kWide = F_WIDE;
-#else
-constexpr uint32_t kWide = 0u;
-#endif
-#ifdef VR_Q4
-constexpr uint32_t kQ4 = F_Q4;
-#else
-constexpr uint32_t kQ4 = 0u;
-#endif
 constexpr uint32_t kFeatAll =
-    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT | kWide | kQ4;
+    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT;
 static_assert((kFeatAll & F_COUNT_EXEC) == 0u, "F_COUNT_EXEC is a compile-time kernel variant, not a scene flag");
 constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH;                                  // C2
 constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                              // C1
@@ -1945,10 +1532,13 @@ constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;      
 template <int STACK, uint32_t FEAT>
 static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
-    if constexpr ((FEAT & F_INLINE_PRIM) == 0u) {
+    // one-frame launches trace the camera ray in the path kernel (a separate
+    // instantiation); the instrumented copy always takes the primary pass
+    if constexpr ((FEAT & (F_INLINE_PRIM | F_COUNT_EXEC)) == 0u) {
         if (p.inline_prim) { launch_wave<STACK, FEAT | F_INLINE_PRIM>(p, n_tiles, s); return; }
-        hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
     }
+    if constexpr ((FEAT & F_INLINE_PRIM) == 0u)
+        hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
     // one resident set: path_waves(STACK, C) waves per SIMD, 4 SIMDs per CU
     constexpr bool C = cornell_kernel<FEAT>();
     constexpr int BT = wave_block(STACK, C), BTS = wave_block_small(STACK, C);
@@ -1962,106 +1552,58 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
                        dim3(BT), 0, s, p);
 }
 
-// F_LDS_TREE launch: the primary pass reads the tree from memory; the path
-// kernel copies it into LDS (the host checks it fits next to the stacks)
-template <uint32_t FEAT>
-static void launch_wave_lt(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
-{
-    if constexpr ((FEAT & F_INLINE_PRIM) == 0u) {
-        if (p.inline_prim) { launch_wave_lt<FEAT | F_INLINE_PRIM>(p, n_tiles, s); return; }
-        hipLaunchKernelGGL((primary_kernel<kLdsTreeStack, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
-    }
-    const size_t dyn = (size_t)p.n_nodes * 32u;
-    static bool attr_set = false;                       // > 64 KB of dynamic LDS: raise the limit once
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&render_wave_kernel_lt<FEAT | F_LDS_TREE>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  kLdsBytesPerCU - kLdsTreeStack * kLdsTreeBlock * 2);
-        attr_set = true;
-    }
-    hipLaunchKernelGGL((render_wave_kernel_lt<FEAT | F_LDS_TREE>), dim3(p.wave_blocks), dim3(kLdsTreeBlock), dyn, s, p);
-}
-
+// One scene specialisation, production (FEAT) or instrumented
+// (FEAT | F_COUNT_EXEC: same launch shape, residency, node-loop threshold and
+// queues as the production kernel of the same scene, plus load counters).
 template <uint32_t FEAT>
 static void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
 {
-#ifndef VR_MIN_SPEC_STACK
-#define VR_MIN_SPEC_STACK 16
-#endif
-    // mesh scenes: the path-pool kernel (traversal divergence); sphere-only
-    // scenes: one pixel per thread, primary hit shared by its paths
-#ifdef VR_CLASSIC_KERNEL
-    const bool wave = false;
-#else
-    const bool wave = (FEAT & F_MESH) != 0 && (p.flags & F_MESH) != 0;
-#endif
-    const uint32_t blocks = n_tiles * p.split;
-    if (!wave)
-        hipLaunchKernelGGL((render_kernel<16, false, FEAT>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-#ifdef VR_Q4
-    else if ((p.flags & F_Q4) != 0u)
-        launch_wave<kQ4Stack, FEAT | F_Q4>(p, n_tiles, s);
-#endif
-    else if ((p.flags & F_LDS_TREE) != 0u)
-        launch_wave_lt<FEAT>(p, n_tiles, s);
-    else if (stack_depth <= 16 && VR_MIN_SPEC_STACK <= 16)
-        launch_wave<16, FEAT>(p, n_tiles, s);
-    else if (stack_depth <= 24 && VR_MIN_SPEC_STACK <= 24)
-        launch_wave<24, FEAT>(p, n_tiles, s);
-    else
-        launch_wave<32, FEAT>(p, n_tiles, s);
+    constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;
+    if constexpr ((FEAT & F_MESH) == 0u) {
+        // sphere-only scenes: one pixel per thread, primary hit shared by its paths
+        hipLaunchKernelGGL((render_kernel<16, CNT, FEAT>), dim3(n_tiles * p.split), dim3(kBlockThreads), 0, s, p);
+    } else {
+        // mesh scenes: the path-pool kernel (traversal divergence)
+        if ((p.flags & F_MESH) == 0u)
+            hipLaunchKernelGGL((render_kernel<16, CNT, FEAT>), dim3(n_tiles * p.split), dim3(kBlockThreads), 0, s, p);
+        else if (stack_depth <= 16)
+            launch_wave<16, FEAT>(p, n_tiles, s);
+        else if (stack_depth <= 24)
+            launch_wave<24, FEAT>(p, n_tiles, s);
+        else
+            launch_wave<32, FEAT>(p, n_tiles, s);
+    }
 }
 
-// The instrumented production kernels: the generic feature set plus
-// F_COUNT_EXEC, in the launch shape launch_spec gives the named ones.
-static void launch_exec_counted(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
+// Scene flags -> specialisation; X = 0 (production) or F_COUNT_EXEC.
+template <uint32_t X>
+static void launch_scene(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
 {
-    constexpr uint32_t FE = kFeatAll | F_COUNT_EXEC;
-    if ((p.flags & F_MESH) == 0u)
-        hipLaunchKernelGGL((render_kernel<16, true, FE>), dim3(n_tiles * p.split), dim3(kBlockThreads), 0, s, p);
-#ifdef VR_Q4
-    else if ((p.flags & F_Q4) != 0u)
-        launch_wave<kQ4Stack, FE>(p, n_tiles, s);
-#endif
-    else if ((p.flags & F_LDS_TREE) != 0u)
-        launch_wave_lt<FE>(p, n_tiles, s);
-    else if (stack_depth <= 16)
-        launch_wave<16, FE>(p, n_tiles, s);
-    else if (stack_depth <= 24)
-        launch_wave<24, FE>(p, n_tiles, s);
-    else if (stack_depth <= 32)
-        launch_wave<32, FE>(p, n_tiles, s);
-    else
-        launch_wave<64, FE>(p, n_tiles, s);
+    const uint32_t need = p.flags & kFeatAll;
+    if (need == kFeatCornellMesh) launch_spec<kFeatCornellMesh | F_EXACT | X>(p, n_tiles, stack_depth, s);
+    else if (need == kFeatCornellSphere) launch_spec<kFeatCornellSphere | F_EXACT | X>(p, n_tiles, stack_depth, s);
+    else if (need == kFeatHdriMesh) launch_spec<kFeatHdriMesh | F_EXACT | X>(p, n_tiles, stack_depth, s);
+    else if (need == kFeatHdriMeshTex) launch_spec<kFeatHdriMeshTex | F_EXACT | X>(p, n_tiles, stack_depth, s);
+    else if (need == kFeatHdriBrdfSphere) launch_spec<kFeatHdriBrdfSphere | F_EXACT | X>(p, n_tiles, stack_depth, s);
+    else launch_spec<kFeatAll | X>(p, n_tiles, stack_depth, s);
 }
 
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int count, void* stream)
 {
     if (n_tiles == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    const uint32_t need = p.flags & kFeatAll & ~kQ4;      // F_Q4 picks the walk inside launch_spec
     const uint32_t blocks = n_tiles * p.split;   // split == 1 for the counting variant
-    if (count == 2) {
-        launch_exec_counted(p, n_tiles, stack_depth, s);
-    } else if (count || stack_depth > 32) {
-        if (count) {
-            if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-            else hipLaunchKernelGGL((render_kernel<64, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
-        } else {
-            launch_wave<64, kFeatAll>(p, n_tiles, s);
-        }
-    } else if (need == kFeatCornellMesh) {
-        launch_spec<kFeatCornellMesh | F_EXACT>(p, n_tiles, stack_depth, s);
-    } else if (need == kFeatCornellSphere) {
-        launch_spec<kFeatCornellSphere | F_EXACT>(p, n_tiles, stack_depth, s);
-    } else if (need == kFeatHdriMesh) {
-        launch_spec<kFeatHdriMesh | F_EXACT>(p, n_tiles, stack_depth, s);
-    } else if (need == kFeatHdriMeshTex) {
-        launch_spec<kFeatHdriMeshTex | F_EXACT>(p, n_tiles, stack_depth, s);
-    } else if (need == kFeatHdriBrdfSphere) {
-        launch_spec<kFeatHdriBrdfSphere | F_EXACT>(p, n_tiles, stack_depth, s);
+    if (count == 1) {
+        // the reference algorithm's event counts (strict traversal, no primary-hit reuse)
+        if (stack_depth <= 32) hipLaunchKernelGGL((render_kernel<32, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+        else hipLaunchKernelGGL((render_kernel<64, true, kFeatAll>), dim3(blocks), dim3(kBlockThreads), 0, s, p);
+    } else if (stack_depth > 32) {
+        if (count) launch_wave<64, kFeatAll | F_COUNT_EXEC>(p, n_tiles, s);
+        else launch_wave<64, kFeatAll>(p, n_tiles, s);
+    } else if (count == 2) {
+        launch_scene<F_COUNT_EXEC>(p, n_tiles, stack_depth, s);
     } else {
-        launch_spec<kFeatAll>(p, n_tiles, stack_depth, s);
+        launch_scene<0u>(p, n_tiles, stack_depth, s);
     }
     return (int)hipGetLastError();
 }

@@ -22,26 +22,16 @@ enum Flags : uint32_t {
     F_TEX_NORM = 1u << 6,    // kHasNormalMap       (:26)
     F_TEX_SPEC = 1u << 7,    // kHasSpecularMap     (:27)
     F_STRICT = 1u << 8,      // visit every pierced box, as the reference (no t-culling)
-    F_WIDE = 1u << 9,        // culled traversal over the 4-wide collapse of the tree (bvh4)
     // compile-time only (never in RenderParams::flags): the instrumented copy
     // of the production kernels (vrhip_render_profiled) -- same algorithm,
     // launch shape and results, plus per-lane counts of the memory operations
     // they execute
     F_COUNT_EXEC = 1u << 10,
-    F_Q4 = 1u << 11,         // culled traversal over the quantized 4-wide nodes (bvhq)
-    F_LDS_TREE = 1u << 12,   // culled traversal with the whole fp16 tree in each block's LDS
     // compile-time only: the path kernel of launches with RenderParams::inline_prim
     // (paths trace their own camera ray; a separate instantiation, so the
     // multi-frame kernels keep the registers that code would take)
     F_INLINE_PRIM = 1u << 13,
 };
-// LDS-resident tree walk: one 1024-thread block per CU (4 waves/SIMD), the
-// fp16 tree (32 B per node) in dynamic LDS next to 16-bit stacks of kLdsTreeStack entries
-constexpr int kLdsTreeBlock = 1024;
-constexpr int kLdsTreeStack = 16;
-constexpr int kLdsBytesPerCU = 163840;
-constexpr int kQ4Stack = 26;         // stack class of the quantized 4-wide walk: 3 pushes per level, depth <= 8
-
 constexpr int kMaxFramesPerLaunch = 64;
 
 // counting variants, slots [0, kCounters): rays, node visits, vert0 slot
@@ -106,12 +96,7 @@ struct RenderParams {
     uint32_t n_queues;               // render_wave_kernel: work queue heads in use (VR_QUEUES / VR_QUEUES_LARGE)
     uint32_t inline_prim;            // paths trace their own camera ray (no primary_kernel pass; F_INLINE_PRIM kernel)
     const vr4* bvh;
-    const vr4* bvh4;                 // 4-wide nodes, 7 rows each (culled traversal, VR_BVH4)
-    uint32_t n_nodes4;
     const vr4* bvh16;                // same nodes, conservative fp16 boxes, 32 B each (culled traversal)
-    const uint32_t* bvhq;            // quantized 4-wide nodes, 48 B each (F_Q4; vrhip_api.cpp build_nodes_q4)
-    uint32_t n_nodesq;
-    uint32_t q4_ebias;               // biased IEEE exponent of a stored scale exponent 0
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
     const vr3* verts;                // 3 vertices per triangle, compact leaf order (face normal at shading)
     const vr3* tri_e;                // per triangle (v0, v1 - v0, v2 - v0): the traversal's copy

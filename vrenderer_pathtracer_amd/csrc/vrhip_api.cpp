@@ -78,10 +78,9 @@ struct vrhip_ctx {
     bool cornell = false, example = false, view_brdf = false;
     bool strict = false;          // exact reference traversal (no t-culling)
     // mesh
-    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr4* bvh4 = nullptr; uint32_t* bvhq = nullptr; vr3* verts = nullptr; vr3* tri_e = nullptr; unsigned long long* tpath = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
+    vr4* bvh = nullptr; vr4* bvh16 = nullptr; vr3* verts = nullptr; vr3* tri_e = nullptr; unsigned long long* tpath = nullptr; vr4* normals = nullptr; vr4* tangents = nullptr; vr2* uvs = nullptr;
     size_t n_bvh = 0, n_slots = 0;
-    uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0, dev_nodes4 = 0;
-    uint32_t dev_nodesq = 0, q4_depth = 0, q4_ebias = 0;    // quantized 4-wide nodes (0 nodes: not built)
+    uint32_t bvh_depth = 0, bvh_nodes = 0, dev_nodes = 0, dev_tris = 0;
     bool mesh = false;
     // environment / textures / brdf
     vr4* hdr = nullptr; uint32_t hdr_w = 0, hdr_h = 0;
@@ -118,8 +117,9 @@ struct vrhip_ctx {
     std::deque<std::pair<hipEvent_t, hipEvent_t>> kev_pending;
     std::vector<hipEvent_t> kev_free;
     bool timed = false;          // ev0/ev1 hold the last render
-    double kernel_ms_total = 0.0;
+    double kernel_ms_total = 0.0;    // union of the launches' render-kernel spans (overlapping launches count once)
     uint64_t launches_total = 0;
+    hipEvent_t kev_last_end = nullptr;   // end event of the latest-ending span accounted so far
     unsigned long long* counters = nullptr;
     // GL interop (colour, depth textures registered by the display host)
     hipGraphicsResource_t gl_res[2] = { nullptr, nullptr };
@@ -128,6 +128,7 @@ struct vrhip_ctx {
     uint8_t* comm_send = nullptr;    // this rank's packed tiles (largest element, 16 B/pixel)
     uint8_t* comm_recv = nullptr;    // rank 0: n_ranks packed buffers, comm_slot bytes apart
     size_t comm_slot = 0;            // bytes per rank slot (max owned pixels x 16 B)
+    uint32_t comm_rank = 0, comm_n = 0;   // the communicator's rank and size (tiling fixed while it exists)
 };
 
 namespace {
@@ -167,9 +168,6 @@ uint32_t owned_tiles_of(uint32_t W, uint32_t H, uint32_t rank, uint32_t n_ranks)
 struct DeviceMesh {
     std::vector<vr4> nodes, normals, tangents;
     std::vector<vr4> nodes16;        // 2 x 16 B per node: conservative fp16 boxes + child indices
-    std::vector<vr4> nodes4;         // 4-wide nodes, 7 x 16 B each (collapsed binary tree)
-    std::vector<uint32_t> nodesq;    // quantized 4-wide nodes, 12 dwords (48 B) each
-    uint32_t q4_depth = 0, q4_ebias = 0;
     std::vector<vr3> tris;           // packed 12 B vertices (vertex .w never reaches a result)
     std::vector<vr3> tri_e;          // per triangle v0, v1 - v0, v2 - v0 (fp32, the kernel's own subtractions)
     std::vector<unsigned long long> tpath;   // per triangle: leaf path from the root under a leading 1 bit
@@ -343,189 +341,6 @@ void build_nodes16(DeviceMesh& dm)
     }
 }
 
-// 4-wide collapse of the binary tree for the t-culled traversal: a 4-node
-// holds the grandchildren of a binary node (a child that is a leaf is kept
-// as is), with the exact fp32 boxes the binary parents store.  Layout per
-// node (7 rows): lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] child[4];
-// child >= 0: 4-node index * 7 (row offset); < 0: leaf code; empty slots
-// hold the sentinel 0x76543210 and are masked out by the traversal.
-void build_nodes4(DeviceMesh& dm)
-{
-    const size_t n = dm.nodes.size() / 4;
-    dm.nodes4.clear();
-    if (n == 0) return;
-    struct Child { float lo[3], hi[3]; int32_t idx; };
-    auto bin_child = [&](size_t node, int ch) {
-        Child c;
-        const vr4 a = dm.nodes[4 * node + ch], z = dm.nodes[4 * node + 2], ni = dm.nodes[4 * node + 3];
-        c.lo[0] = a.x; c.hi[0] = a.y; c.lo[1] = a.z; c.hi[1] = a.w;
-        c.lo[2] = ch ? z.z : z.x; c.hi[2] = ch ? z.w : z.y;
-        std::memcpy(&c.idx, ch ? &ni.y : &ni.x, 4);
-        return c;
-    };
-    std::vector<int32_t> id4(n, -1);          // binary node -> 4-node index
-    std::vector<size_t> queue{ 0 };
-    id4[0] = 0;
-    std::vector<std::array<Child, 4>> kids;
-    std::vector<int> nkids;
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-        const size_t b = queue[qi];
-        std::array<Child, 4> k4;
-        int nk = 0;
-        for (int ch = 0; ch < 2; ++ch) {
-            const Child c = bin_child(b, ch);
-            if (c.idx >= 0) {                 // inner: take its two children
-                const size_t cb = (size_t)c.idx / 4;
-                k4[nk++] = bin_child(cb, 0);
-                k4[nk++] = bin_child(cb, 1);
-            } else {
-                k4[nk++] = c;
-            }
-        }
-        for (int k = 0; k < nk; ++k) {
-            if (k4[k].idx >= 0) {
-                const size_t cb = (size_t)k4[k].idx / 4;
-                if (id4[cb] < 0) { id4[cb] = (int32_t)queue.size(); queue.push_back(cb); }
-            }
-        }
-        kids.push_back(k4);
-        nkids.push_back(nk);
-    }
-    dm.nodes4.assign(7 * queue.size(), vr4{ 0, 0, 0, 0 });
-    for (size_t i = 0; i < queue.size(); ++i) {
-        float* r = &dm.nodes4[7 * i].x;     // 28 floats
-        for (int k = 0; k < 4; ++k) {
-            if (k < nkids[i]) {
-                const Child& c = kids[i][k];
-                for (int a = 0; a < 3; ++a) { r[8 * a + k] = c.lo[a]; r[8 * a + 4 + k] = c.hi[a]; }
-                const int32_t idx = c.idx >= 0 ? 7 * id4[(size_t)c.idx / 4] : c.idx;
-                std::memcpy(&r[24 + k], &idx, 4);
-            } else {
-                for (int a = 0; a < 3; ++a) { r[8 * a + k] = 0.f; r[8 * a + 4 + k] = 0.f; }
-                const int32_t empty = 0x76543210;  // the traversal's sentinel: never entered
-                std::memcpy(&r[24 + k], &empty, 4);
-            }
-        }
-    }
-}
-
-// Quantized 4-wide nodes for the t-culled traversal (default where the stack
-// fits, see render_impl): each node holds the grandchildren of one binary node
-// (a leaf child is kept as is), so a ray visits about half as many nodes, and
-// a node is 48 B -- three 16-B loads:
-//   dword 0: origin.x | origin.y << 16 (IEEE halves, rounded down)
-//   dword 1: origin.z | ex << 16 | ey << 21 | ez << 26 (5-bit scale exponents)
-//   dwords 2..7: lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4] (bytes)
-//   dwords 8..11: child[4]: >= 0 quantized-node index, < 0 leaf code, or the
-//                 traversal's sentinel for an empty slot (never entered).
-// A child box is [origin + lo * s, origin + hi * s] per axis with
-// s = 2^(e + ebias - 127): lows rounded down and highs up, so it contains the
-// exact box and no hit is lost (the equal-t tie-break keeps the result
-// independent of the changed visit order).  ebias is chosen per mesh so that
-// the largest node's exponent is representable; the smallest nodes may get a
-// coarser (still conservative) scale.
-void build_nodes_q4(DeviceMesh& dm)
-{
-    dm.nodesq.clear();
-    dm.q4_depth = 0;
-    const size_t n = dm.nodes.size() / 4;
-    if (n == 0) return;
-    struct Child { float lo[3], hi[3]; int32_t idx; };
-    auto bin_child = [&](size_t node, int ch) {
-        Child c;
-        const vr4 a = dm.nodes[4 * node + ch], z = dm.nodes[4 * node + 2], ni = dm.nodes[4 * node + 3];
-        c.lo[0] = a.x; c.hi[0] = a.y; c.lo[1] = a.z; c.hi[1] = a.w;
-        c.lo[2] = ch ? z.z : z.x; c.hi[2] = ch ? z.w : z.y;
-        std::memcpy(&c.idx, ch ? &ni.y : &ni.x, 4);
-        return c;
-    };
-    auto half_to_float = [](uint16_t h) {
-        const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
-        double f = e == 0 ? std::ldexp((double)m, -24) : (e == 31 ? INFINITY : std::ldexp((double)(m | 0x400u), (int)e - 25));
-        return (h & 0x8000u) ? -f : f;
-    };
-    std::vector<int32_t> qid(n, -1);                 // binary node -> quantized-node index
-    std::vector<size_t> queue{ 0 };
-    std::vector<uint32_t> qdepth{ 1 };
-    qid[0] = 0;
-    std::vector<std::array<Child, 4>> kids;
-    std::vector<int> nkids;
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-        std::array<Child, 4> k4;
-        int nk = 0;
-        for (int ch = 0; ch < 2; ++ch) {
-            const Child c = bin_child(queue[qi], ch);
-            if (c.idx >= 0) { k4[nk++] = bin_child((size_t)c.idx / 4, 0); k4[nk++] = bin_child((size_t)c.idx / 4, 1); }
-            else k4[nk++] = c;
-        }
-        for (int k = 0; k < nk; ++k) {
-            if (k4[k].idx < 0) continue;
-            const size_t cb = (size_t)k4[k].idx / 4;
-            if (qid[cb] < 0) { qid[cb] = (int32_t)queue.size(); queue.push_back(cb); qdepth.push_back(qdepth[qi] + 1); }
-        }
-        kids.push_back(k4);
-        nkids.push_back(nk);
-        dm.q4_depth = std::max(dm.q4_depth, qdepth[qi]);
-    }
-    // origins (fp16, rounded down) and the smallest scale exponent per axis
-    const size_t nq = queue.size();
-    std::vector<std::array<uint16_t, 3>> org(nq);
-    std::vector<std::array<int, 3>> expo(nq);
-    int max_e = -126;
-    for (size_t i = 0; i < nq; ++i) {
-        for (int a = 0; a < 3; ++a) {
-            float lo = INFINITY, hi = -INFINITY;
-            for (int k = 0; k < nkids[i]; ++k) { lo = std::min(lo, kids[i][k].lo[a]); hi = std::max(hi, kids[i][k].hi[a]); }
-            org[i][a] = half_bits_directed(lo, false);
-            if (!(std::fabs(lo) < 60000.f) || !(std::fabs(hi) < 60000.f)) {   // beyond fp16 origins: binary nodes only
-                dm.nodesq.clear();
-                dm.q4_depth = 0;
-                return;
-            }
-            const double ext = (double)hi - half_to_float(org[i][a]);
-            int e = -126;
-            if (ext > 0.0) {
-                e = (int)std::ceil(std::log2(ext / 255.0));
-                while (std::ldexp(255.0, e) < ext) ++e;
-                while (e > -126 && std::ldexp(255.0, e - 1) >= ext) --e;
-            }
-            expo[i][a] = std::max(e, -126);
-            max_e = std::max(max_e, expo[i][a]);
-        }
-    }
-    const int ebias = std::max(max_e - 31, -126) + 127;   // biased IEEE exponent of stored exponent 0
-    dm.q4_ebias = (uint32_t)ebias;
-    dm.nodesq.assign(12 * nq, 0u);
-    for (size_t i = 0; i < nq; ++i) {
-        uint32_t* w = &dm.nodesq[12 * i];
-        int d[3];
-        double origin[3], scale[3];
-        for (int a = 0; a < 3; ++a) {
-            d[a] = std::max(expo[i][a] + 127 - ebias, 0);          // coarser for the very smallest nodes
-            origin[a] = half_to_float(org[i][a]);
-            scale[a] = std::ldexp(1.0, d[a] + ebias - 127);
-        }
-        w[0] = (uint32_t)org[i][0] | ((uint32_t)org[i][1] << 16);
-        w[1] = (uint32_t)org[i][2] | ((uint32_t)d[0] << 16) | ((uint32_t)d[1] << 21) | ((uint32_t)d[2] << 26);
-        for (int k = 0; k < 4; ++k) {
-            int32_t idx = 0x76543210;                               // empty slot: the sentinel
-            if (k < nkids[i]) {
-                const Child& c = kids[i][k];
-                idx = c.idx >= 0 ? qid[(size_t)c.idx / 4] : c.idx;
-                for (int a = 0; a < 3; ++a) {
-                    const double ql = std::floor(((double)c.lo[a] - origin[a]) / scale[a]);
-                    const double qh = std::ceil(((double)c.hi[a] - origin[a]) / scale[a]);
-                    const uint32_t bl = (uint32_t)std::min(std::max(ql, 0.0), 255.0);
-                    const uint32_t bh = (uint32_t)std::min(std::max(qh, 0.0), 255.0);
-                    w[2 + 2 * a] |= bl << (8 * k);
-                    w[3 + 2 * a] |= bh << (8 * k);
-                }
-            }
-            std::memcpy(&w[8 + k], &idx, 4);
-        }
-    }
-}
-
 bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const vr4* normals,
                       const vr4* tangents, const vr2* uvs, DeviceMesh& dm, std::string& why)
 {
@@ -572,12 +387,8 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
         }
     }
     tri_paths(dm);
-#ifndef VR_NO_AREA_ORDER
     order_nodes_by_area(dm);
-#endif
     build_nodes16(dm);
-    build_nodes4(dm);
-    build_nodes_q4(dm);
     if (dm.tris.empty()) {
         dm.tris.push_back(vr3{ 0, 0, 0 });
         dm.normals.push_back(vr4{ 0, 0, 0, 0 });
@@ -699,7 +510,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     quiesce(c);
     dfree(c->accum); dfree(c->rgba); dfree(c->depth); dfree(c->cam_sxy);
-    dfree(c->bvh); dfree(c->bvh16); dfree(c->bvh4); dfree(c->bvhq); dfree(c->verts); dfree(c->tri_e); dfree(c->tpath); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
+    dfree(c->bvh); dfree(c->bvh16); dfree(c->verts); dfree(c->tri_e); dfree(c->tpath); dfree(c->normals); dfree(c->tangents); dfree(c->uvs);
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     for (int i = 0; i < 2; ++i)
         if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
@@ -717,6 +528,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (auto& pr : c->kev_pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (hipEvent_t e : c->kev_free) (void)hipEventDestroy(e);
+    if (c->kev_last_end) (void)hipEventDestroy(c->kev_last_end);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return VRHIP_OK;
@@ -781,11 +593,6 @@ int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, cons
     const size_t nt = dm.tris.size();
     if ((rc = upload(c, c->bvh, dm.nodes.data(), dm.nodes.size() * 16))) return rc;
     if ((rc = upload(c, c->bvh16, dm.nodes16.data(), dm.nodes16.size() * 16))) return rc;
-    if ((rc = upload(c, c->bvh4, dm.nodes4.data(), dm.nodes4.size() * 16))) return rc;
-    c->dev_nodes4 = (uint32_t)(dm.nodes4.size() / 7);
-    if ((rc = upload(c, c->bvhq, dm.nodesq.data(), dm.nodesq.size() * 4))) return rc;
-    c->dev_nodesq = (uint32_t)(dm.nodesq.size() / 12);
-    c->q4_depth = dm.q4_depth; c->q4_ebias = dm.q4_ebias;
     if ((rc = upload(c, c->verts, dm.tris.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->tri_e, dm.tri_e.data(), nt * sizeof(vr3)))) return rc;
     if ((rc = upload(c, c->tpath, dm.tpath.data(), dm.tpath.size() * sizeof(unsigned long long)))) return rc;
@@ -931,7 +738,7 @@ int vrhip_gl_present(vrhip_ctx* c)
 }
 
 #if defined(VR_WAVE_TIMES) && defined(VR_PATH_TIMES)
-constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192 + 2 * (int)vr::kPathTimesCap;   // + 2 per path
+constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192 + 3 * (int)vr::kPathTimesCap;   // + 3 per path
 #elif defined(VR_WAVE_TIMES)
 constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192;   // + per-wave start / end / paths of render_wave_kernel
 #else
@@ -950,6 +757,9 @@ static int ensure_counters(vrhip_ctx* c)
 // Adds the render-kernel times of completed launches to the totals; with
 // `wait`, waits for all of them.  Never blocks otherwise, so a render call
 // does not wait for the previous one (launches pipeline, see render_impl).
+// Launches on the path streams can overlap: the total is the union of the
+// spans (each span counted from the later of its start and the latest end
+// accounted before it), so it never exceeds the wall time they cover.
 static int account_pending(vrhip_ctx* c, bool wait)
 {
     while (!c->kev_pending.empty()) {
@@ -963,11 +773,24 @@ static int account_pending(vrhip_ctx* c, bool wait)
         }
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+        bool newest_end = true;
+        if (c->kev_last_end) {
+            float gap = 0.f, ext = 0.f;          // start and end relative to the latest end so far
+            HIP_TRY(hipEventElapsedTime(&gap, c->kev_last_end, pr.first));
+            HIP_TRY(hipEventElapsedTime(&ext, c->kev_last_end, pr.second));
+            if (gap < 0.f) ms = ext > 0.f ? ext : 0.f;     // starts inside the covered time
+            newest_end = ext > 0.f;
+        }
         c->kernel_ms_total += ms;
         c->launches_total += 1;
         c->kev_pending.pop_front();
         c->kev_free.push_back(pr.first);
-        c->kev_free.push_back(pr.second);
+        if (newest_end) {
+            if (c->kev_last_end) c->kev_free.push_back(c->kev_last_end);
+            c->kev_last_end = pr.second;
+        } else {
+            c->kev_free.push_back(pr.second);
+        }
     }
     return VRHIP_OK;
 }
@@ -1053,24 +876,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     if (c->example) f |= vr::F_EXAMPLE;
     if (c->view_brdf) f |= vr::F_VIEW_BRDF;
     if (c->strict) f |= vr::F_STRICT;
-#ifdef VR_BVH4
-    if (!c->strict && c->mesh && c->bvh_depth <= 30) f |= vr::F_WIDE;   // <= 3 pushes per 4-wide level
-#endif
     if (c->mesh) f |= vr::F_MESH;
-#ifdef VR_LDS_TREE
-    // opt-in (C2 -19 %, C3 -11 % at 4 waves/SIMD: DESIGN.md): the whole conservative-fp16 tree in each path-kernel block's LDS when it
-    // fits next to the 16-bit stacks of a 1,024-thread block (the 10k-triangle
-    // knot: 3,724 nodes x 32 B = 119 KB); depth <= 15 for the 16-entry stacks
-    if (!c->strict && c->mesh && c->bvh_depth <= 15 &&
-        (size_t)c->dev_nodes * 32u + (size_t)vr::kLdsTreeStack * vr::kLdsTreeBlock * 2u + 1024u <= (size_t)vr::kLdsBytesPerCU)
-        f |= vr::F_LDS_TREE;
-#endif
-#ifdef VR_Q4
-    // quantized 4-wide walk (opt-in: 43 % fewer node visits and 9 % fewer lane
-    // loads on C2, but 11 % slower -- DESIGN.md); <= 3 pushes per level in kQ4Stack
-    if (!c->strict && c->mesh && c->dev_nodesq > 0 && 3 * c->q4_depth + 1 <= (uint32_t)vr::kQ4Stack)
-        f |= vr::F_Q4;
-#endif
     if (c->brdf) f |= vr::F_BRDF;
     if (c->tex[0]) f |= vr::F_TEX_DIFF;
     if (c->tex[1]) f |= vr::F_TEX_NORM;
@@ -1078,38 +884,32 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.flags = f;
     p.tiles_x = p.wr / 16u;
     p.rank = c->rank; p.nranks = c->nranks;
-    p.bvh4 = c->bvh4; p.n_nodes4 = c->mesh ? c->dev_nodes4 : 0;
-    p.bvhq = c->bvhq; p.n_nodesq = c->mesh ? c->dev_nodesq : 0; p.q4_ebias = c->q4_ebias;
     p.bvh = c->bvh; p.bvh16 = c->bvh16; p.n_nodes = c->mesh ? c->dev_nodes : 0; p.verts = c->verts; p.tri_e = c->tri_e; p.tpath = c->tpath; p.n_tris = c->mesh ? c->dev_tris : 0; p.normals = c->normals; p.tangents = c->tangents; p.uvs = c->uvs;
     p.hdr = c->hdr; p.hdr_w = c->hdr_w; p.hdr_h = c->hdr_h;
     for (int i = 0; i < 3; ++i) { p.tex[i] = c->tex[i]; p.tex_w[i] = c->tex_w[i]; p.tex_h[i] = c->tex_h[i]; }
     p.brdf = c->brdf;
     p.accum = c->accum; p.rgba = c->rgba; p.depth = c->depth;
     const uint32_t n_tiles = owned_tiles_of(c->W, c->H, c->rank, c->nranks);
-    // stack entries needed: binary walk depth + 1; 4-wide walk 3 per 4-level + 1
-    const int stack = (f & vr::F_WIDE) ? (c->bvh_depth <= 15 ? 32 : 64)
-                                       : (c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 23 ? 24 : c->bvh_depth <= 30 ? 32 : 64);
+    // stack entries needed: walk depth + 1
+    const int stack = c->bvh_depth <= 15 ? 16 : c->bvh_depth <= 23 ? 24 : c->bvh_depth <= 30 ? 32 : 64;
     if (count) {
         if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kDebugSlots, c->stream));
         p.counters = c->counters;
     }
-#if defined(VR_TIMING) || defined(VR_LANESTATS) || defined(VR_NODE_STAMPS) || defined(VR_WAVE_TIMES)
+#if defined(VR_WAVE_TIMES)
     if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
-    p.counters = c->counters;   // diagnostic build: phase timers in slots 8..13
+    p.counters = c->counters;   // diagnostic build: per-wave / per-path records
 #endif
     if ((rc = account_pending(c, false)) != VRHIP_OK) return rc;
     const uint32_t k_max = std::min<uint32_t>(n_frames, (uint32_t)vr::kMaxFramesPerLaunch);
     const uint32_t split_max = count == 1 ? 1u : choose_split(c, n_tiles, k_max);
     p.path_stride = n_tiles * (uint32_t)vr::kBlockThreads;
-    p.use_scratch = count == 1 ? 0u : 1u;   // the reference counting variant accumulates in place
     const size_t need = (size_t)2 * k_max * p.path_stride;   // scratch float4s of the largest launch
-    if (p.use_scratch) {
-        // the path-pool kernel is persistent: one resident set of blocks per
-        // CU (the launcher sizes it from the kernel's occupancy) draining the
-        // work queues
-        p.wave_blocks = c->cu_count;
-    }
+    // the path-pool kernel is persistent: one resident set of blocks per CU
+    // (the launcher sizes it from the kernel's occupancy) draining the work queues
+    p.wave_blocks = c->cu_count;
+    const bool wave_kernel = (f & vr::F_MESH) != 0u;   // mesh scenes: the path-pool kernel (scratch + finish pass)
     (void)hipGetLastError();            // launches below report their own errors only
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     uint32_t done = 0;
@@ -1118,6 +918,11 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         p.first_frame = c->frame;
         p.n_frames = k;
         p.split = std::min<uint32_t>(split_max, 2u * k);
+        // the reference counting variant, and sphere-only launches whose
+        // pixels run all their paths in one thread (split 1), accumulate in
+        // registers in path order (render_kernel's direct mode): no scratch
+        // round trip, no finish pass
+        p.use_scratch = (count == 1 || (!wave_kernel && p.split == 1u)) ? 0u : 1u;
         for (uint32_t i = 0; i < k; ++i) p.times[i] = times ? times[done + i] : time_seed;
         // Path launches take the VR_PATH_STREAMS path streams in turn: launch
         // i's render kernels wait only for the finish pass of launch i - 3
@@ -1134,7 +939,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // device (one frame per synchronous call) runs its render and finish
         // kernels on `stream` with no cross-stream waits
         const bool in_flight = done > 0 || (c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
-        const bool ovl = c->overlap > 0 || (c->overlap < 0 && small && in_flight);
+        // counting launches never overlap: their counters are zeroed on
+        // `stream` (above), which a path stream would not wait for
+        const bool ovl = count == 0 && (c->overlap > 0 || (c->overlap < 0 && small && in_flight));
         p.small_blocks = small ? 1u : 0u;
         p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
         p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? (c->cornell ? VR_QUEUES : VR_QUEUES_HDRI)
@@ -1294,7 +1101,11 @@ int vrhip_kernel_stats(vrhip_ctx* c, double* total_ms, uint64_t* launches, int r
     if ((rc = account_pending(c, true)) != VRHIP_OK) return rc;
     if (total_ms) *total_ms = c->kernel_ms_total;
     if (launches) *launches = c->launches_total;
-    if (reset) { c->kernel_ms_total = 0.0; c->launches_total = 0; }
+    if (reset) {
+        c->kernel_ms_total = 0.0;
+        c->launches_total = 0;
+        if (c->kev_last_end) { c->kev_free.push_back(c->kev_last_end); c->kev_last_end = nullptr; }
+    }
     return VRHIP_OK;
 }
 
@@ -1338,6 +1149,10 @@ int vrhip_device_buffers(vrhip_ctx* c, void** accum, void** rgba8, void** depth8
 int vrhip_set_tiling(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks)
 {
     if (!c || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad tiling");
+    // the gather buffers and the RCCL communicator are sized for the
+    // communicator's tiling: it cannot change while they exist
+    if (c->comm && (rank != c->comm_rank || n_ranks != c->comm_n))
+        return fail(VRHIP_ERR_INVALID, "tiling is fixed while a communicator exists (vrhip_comm_destroy first)");
     quiesce(c);
     c->rank = rank; c->nranks = n_ranks;
     return VRHIP_OK;
@@ -1437,6 +1252,7 @@ int vrhip_comm_init(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks, const uint8_t
     if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
     dfree(c->comm_send); dfree(c->comm_recv);
     if ((rc = vrhip_set_tiling(c, rank, n_ranks)) != VRHIP_OK) return rc;
+    c->comm_rank = rank; c->comm_n = n_ranks;
     c->comm_slot = (size_t)max_owned_pixels(c->W, c->H, n_ranks) * 16u;
     const size_t slot = c->comm_slot ? c->comm_slot : 16u;
     if (hipMalloc((void**)&c->comm_send, slot) != hipSuccess ||
@@ -1456,7 +1272,10 @@ int vrhip_comm_gather(vrhip_ctx* c, int what)
     int rc = set_device(c); if (rc) return rc;
     // pack -> gather -> (rank 0) unpack, all on the context stream, behind the
     // finish passes that wrote the images
+    if (c->rank != c->comm_rank || c->nranks != c->comm_n)
+        return fail(VRHIP_ERR_INVALID, "tiling differs from the communicator's");
     const size_t bytes = (size_t)max_owned_pixels(c->W, c->H, c->nranks) * (size_t)elem_size(what);
+    if (bytes > c->comm_slot) return fail(VRHIP_ERR_INVALID, "gather payload exceeds the communicator's buffers");
     if ((rc = vrhip_pack_tiles(c, what, c->comm_send)) != VRHIP_OK) return rc;
     const ncclResult_t r = ncclGather(c->comm_send, c->comm_recv, bytes, ncclUint8, 0, c->comm, c->stream);
     if (r != ncclSuccess) return nccl_fail(r, "ncclGather");
