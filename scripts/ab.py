@@ -40,7 +40,20 @@ wr, hr = (sc["width"] // 16) * 16, (sc["height"] // 16) * 16
 paths = wr * hr * 2 * F
 ts.sort()
 med = ts[len(ts) // 2]
-print(json.dumps({{"mpaths": paths / med / 1e6, "best": paths / ts[0] / 1e6,
+inter = None
+if {inter} > 0:      # one frame per synchronous call (the reference's render() cadence)
+    r.clearBuffer()
+    for i in range(3):
+        r.render(frames=1, times=[sc["time"] + 50000 + i])
+    ti = []
+    for b in range(3):
+        t0 = time.perf_counter()
+        for i in range({inter}):
+            r.render(frames=1, times=[sc["time"] + 60000 + b * 1000 + i])
+        ti.append((time.perf_counter() - t0) / {inter})
+    ti.sort()
+    inter = ti[1] * 1e3
+print(json.dumps({{"mpaths": paths / med / 1e6, "best": paths / ts[0] / 1e6, "inter_ms": inter,
                    "hash": int(np.bitwise_xor.reduce(acc.view(np.uint32).reshape(-1)))}}))
 """
 
@@ -53,6 +66,7 @@ def main():
     ap.add_argument("--strict", action="store_true")
     ap.add_argument("--leaf", type=int, default=None, help="max triangles per leaf of the scene's BVH")
     ap.add_argument("--node-cost", type=float, default=None, help="SAH node cost of the scene's BVH")
+    ap.add_argument("--interactive", type=int, default=0, help="also time N one-frame synchronous calls (median of 3)")
     ap.add_argument("--overlap", default="", help="comma-separated vrhip_set_overlap modes to run per library (1, 0, -1)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
@@ -64,7 +78,8 @@ def main():
             env["VRHIP_MAX_LEAF"] = str(a.leaf)
         if a.node_cost is not None:
             env["VRHIP_SAH_NODE_COST"] = str(a.node_cost)
-        code = CHILD.format(repo=REPO, cfg=a.cfg, frames=a.frames, steps=a.steps, strict=a.strict, overlap=ov)
+        code = CHILD.format(repo=REPO, cfg=a.cfg, frames=a.frames, steps=a.steps, strict=a.strict, overlap=ov,
+                            inter=a.interactive)
         p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
         if p.returncode != 0:
             print(f"{lib}: FAILED rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
@@ -74,7 +89,8 @@ def main():
         res = json.loads(p.stdout.strip().splitlines()[-1])
         name = os.path.basename(lib) + (f" overlap={ov}" if ov else "")
         results[name] = res
-        print(f"{name:40s} {res['mpaths']:9.1f} Mpaths/s (best {res['best']:.1f})  hash {res['hash']:#x}",
+        it = f"  one frame/call {res['inter_ms']:.4f} ms" if res.get("inter_ms") else ""
+        print(f"{name:40s} {res['mpaths']:9.1f} Mpaths/s (best {res['best']:.1f}){it}  hash {res['hash']:#x}",
               flush=True)
     hashes = {v["hash"] for v in results.values()}
     print("all results identical" if len(hashes) == 1 else f"RESULTS DIFFER: {len(hashes)} distinct hashes")

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Drain diagnostics of the path kernel: per-wave timelines (scripts/wave_times.py)
 # and per-path records (scripts/path_times.py) of a -DVR_WAVE_TIMES -DVR_PATH_TIMES
-# build (scripts/build_variants.sh pt="-DVR_WAVE_TIMES -DVR_PATH_TIMES").
+# build (scripts/build_variants.sh pt="-DVR_WAVE_TIMES -DVR_PATH_TIMES -DVR_PATH_COUNTS"; ptl: the same without -DVR_PATH_COUNTS, fewer registers).
 #   bash scripts/gpu_wt.sh <variant> "C2 1;C3 1"
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 V=${1:-pt}; RUNS=${2:-"C2 1;C3 1"}

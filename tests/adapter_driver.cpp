@@ -1,15 +1,36 @@
 // Drives integration/vRendererHIP through the vRenderer interface the way
-// NGLScene does (src/NGLScene.cpp:82-89,196-197,224,259,443-456), with
+// NGLScene does (src/NGLScene.cpp:82-89,196-197,205-231,259,345-457), with
 // stand-in Camera/GL implementations.  Writes the last RGBA8 image uploaded
 // to the colour texture and the frame count to argv[1].
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "vRendererHIP.h"
+
+// loadBRDF takes ownership of the table and delete[]s it, as
+// src/vRendererCuda.cpp:430 does: count the array deletions of that pointer
+static const void *g_watch = nullptr;
+static int g_watch_deleted = 0;
+void operator delete[](void *p) noexcept
+{
+  if(p && p == g_watch)
+    ++g_watch_deleted;
+  std::free(p);
+}
+void operator delete[](void *p, std::size_t) noexcept { operator delete[](p); }
+void *operator new[](std::size_t n)
+{
+  void *p = std::malloc(n ? n : 1);
+  if(!p)
+    throw std::bad_alloc();
+  return p;
+}
 
 static std::vector<unsigned char> g_colour;
 static GLuint g_bound = 0;
@@ -20,9 +41,6 @@ void glTexSubImage2D(GLenum, GLint, GLint, GLint, GLsizei w, GLsizei h, GLenum, 
   if(g_bound == 1)
     g_colour.assign(static_cast<const unsigned char *>(pixels), static_cast<const unsigned char *>(pixels) + 4 * w * h);
 }
-int QImage::width() const { return 0; }
-int QImage::height() const { return 0; }
-QRgb QImage::pixel(int, int) const { return 0; }
 
 // reference default camera (src/Camera.cpp:11-24,119-123)
 void Camera::consume() {}
@@ -125,13 +143,155 @@ static void writeFlat(FILE *_out, const vRendererHIP::FlatMesh &_flat)
     std::fwrite(v->data(), 4, v->size(), _out);
 }
 
+// ---- scene files (tests/test_adapter.py) ---------------------------------------
+// u32 W, H, frames, cornell, example_sphere, use_brdf, has_mesh
+//   [mesh: as loadMesh]
+// u32 has_hdr [u32 w, h; u16 halves[4wh] (Imf::Rgba)]
+// u32 n_tex  [per texture: u32 type, w, h; f32 gamma; u32 argb[wh] (QRgb)]
+// u32 has_brdf [f32 table[3 * 90 * 90 * 180] (MERL, planar R, G, B)]
+struct Reader
+{
+  FILE *f;
+  bool ok = true;
+  template <typename T> T get() { T v{}; ok = ok && std::fread(&v, sizeof(T), 1, f) == 1; return v; }
+  template <typename T> void get(T *dst, size_t n) { ok = ok && std::fread(dst, sizeof(T), n, f) == n; }
+};
+
+static bool readMeshFrom(Reader &_in, vMeshData &_m)
+{
+  const uint32_t nv = _in.get<uint32_t>(), nt = _in.get<uint32_t>();
+  std::vector<float> pos(3 * nv), nrm(3 * nv), tan(3 * nv), uv(2 * nv);
+  std::vector<uint32_t> tris(3 * nt);
+  _in.get(pos.data(), pos.size()); _in.get(nrm.data(), nrm.size()); _in.get(tan.data(), tan.size());
+  _in.get(uv.data(), uv.size()); _in.get(tris.data(), tris.size());
+  if(!_in.ok)
+    return false;
+  _m.m_vertices.resize(nv);
+  for(uint32_t i = 0; i < nv; ++i)
+  {
+    vHVert &v = _m.m_vertices[i];
+    v.m_vert.m_x = pos[3 * i]; v.m_vert.m_y = pos[3 * i + 1]; v.m_vert.m_z = pos[3 * i + 2];
+    v.m_normal.m_x = nrm[3 * i]; v.m_normal.m_y = nrm[3 * i + 1]; v.m_normal.m_z = nrm[3 * i + 2];
+    v.m_tangent.m_x = tan[3 * i]; v.m_tangent.m_y = tan[3 * i + 1]; v.m_tangent.m_z = tan[3 * i + 2];
+    v.m_u = uv[2 * i]; v.m_v = uv[2 * i + 1];
+  }
+  _m.m_triangles.resize(nt);
+  for(uint32_t t = 0; t < nt; ++t)
+    for(int k = 0; k < 3; ++k)
+      _m.m_triangles[t].m_indices[k] = tris[3 * t + k];
+  _m.m_bvh.m_triIndices.resize(nt);
+  for(uint32_t t = 0; t < nt; ++t)
+    _m.m_bvh.m_triIndices[t] = t;
+  _m.m_bvh.m_root.reset(buildTree(_m, _m.m_bvh.m_triIndices, 0, nt));
+  return true;
+}
+
+// Every ingestion entry point NGLScene calls, in its order: init, register*,
+// setCamera, the toggles, setFresnel*, initMesh, loadHDR (Imf::Rgba halves),
+// loadTexture (QImage, gamma; inverse gamma on diffuse only), loadBRDF (takes
+// ownership), useBRDF; then `frames` render() calls.  Output: frames, the
+// colour texture, whether loadBRDF delete[]d the table exactly once, and the
+// flattened mesh the adapter uploaded (if any).
+static int runSceneFile(const char *_out, const char *_scene)
+{
+  Reader in{ std::fopen(_scene, "rb") };
+  if(!in.f)
+    return 3;
+  const uint32_t W = in.get<uint32_t>(), H = in.get<uint32_t>(), frames = in.get<uint32_t>();
+  const bool cornell = in.get<uint32_t>() != 0, example = in.get<uint32_t>() != 0, useBrdf = in.get<uint32_t>() != 0;
+  vMeshData mesh;
+  const bool hasMesh = in.get<uint32_t>() != 0;
+  if(hasMesh && !readMeshFrom(in, mesh))
+    return 3;
+  std::vector<Imf::Rgba> hdr;
+  uint32_t hw = 0, hh = 0;
+  if(in.get<uint32_t>() != 0)
+  {
+    hw = in.get<uint32_t>(); hh = in.get<uint32_t>();
+    hdr.resize(static_cast<size_t>(hw) * hh);
+    in.get(reinterpret_cast<uint16_t *>(hdr.data()), 4 * hdr.size());
+  }
+  struct Tex { uint32_t type; float gamma; QImage img; };
+  std::vector<Tex> texs(in.get<uint32_t>());
+  for(Tex &t : texs)
+  {
+    t.type = in.get<uint32_t>();
+    const uint32_t w = in.get<uint32_t>(), h = in.get<uint32_t>();
+    t.gamma = in.get<float>();
+    t.img = QImage(static_cast<int>(w), static_cast<int>(h), QImage::Format_ARGB32);
+    std::vector<uint32_t> px(static_cast<size_t>(w) * h);
+    in.get(px.data(), px.size());
+    for(uint32_t y = 0; y < h; ++y)
+      for(uint32_t x = 0; x < w; ++x)
+        t.img.setPixel(static_cast<int>(x), static_cast<int>(y), px[static_cast<size_t>(y) * w + x]);
+  }
+  float *brdf = nullptr;
+  if(in.get<uint32_t>() != 0)
+  {
+    const size_t n = 3u * BRDF_SAMPLING_RES_THETA_H * BRDF_SAMPLING_RES_THETA_D * BRDF_SAMPLING_RES_PHI_D / 2;
+    brdf = new float[n];                      // as vBRDFLoader::loadBinary hands it over
+    in.get(brdf, n);
+  }
+  std::fclose(in.f);
+  if(!in.ok)
+    return 3;
+
+  vRendererHIP r;
+  r.init(W, H);
+  GLuint tex = 1, depth = 2;
+  r.registerTextureBuffer(tex);
+  r.registerDepthBuffer(depth);
+  Camera cam;
+  r.setCamera(&cam);
+  r.useCornellBox(cornell);
+  r.useExampleSphere(example);
+  r.setFresnelCoef(0.1f);
+  r.setFresnelPower(3.f);
+  if(hasMesh)
+    r.initMesh(mesh);
+  if(!hdr.empty())
+    r.loadHDR(hdr.data(), hw, hh);
+  for(const Tex &t : texs)
+    r.loadTexture(t.img, t.gamma, t.type);
+  uint32_t brdfDeleted = 0;
+  if(brdf)
+  {
+    g_watch = brdf;
+    const bool loaded = r.loadBRDF(brdf);
+    brdfDeleted = (loaded && g_watch_deleted == 1) ? 1u : 0u;
+    g_watch = nullptr;
+  }
+  r.useBRDF(useBrdf);
+  r.clearBuffer();
+  for(uint32_t f = 0; f < frames; ++f)
+    r.render();
+  const unsigned int n = r.getFrameCount();
+  r.cleanUp();
+  FILE *out = std::fopen(_out, "wb");
+  std::fwrite(&n, 4, 1, out);
+  std::fwrite(&brdfDeleted, 4, 1, out);
+  std::fwrite(g_colour.data(), 1, g_colour.size(), out);
+  if(hasMesh)
+  {
+    vRendererHIP::FlatMesh flat;
+    vRendererHIP::flattenSBVH(mesh, flat);
+    writeFlat(out, flat);
+  }
+  std::fclose(out);
+  std::printf("frames=%u bytes=%zu brdf_deleted=%u\n", n, g_colour.size(), brdfDeleted);
+  return 0;
+}
+
 // usage: adapter_driver <out>                      Cornell + example sphere, 64x64, 3 frames
+//        adapter_driver <out> --scene <file>       a scene file (above) through every ingestion call
 //        adapter_driver <out> <mesh> [--flatten]   Cornell + the mesh (its SBVH flattened by the
 //                                                  adapter); --flatten: only write the flat arrays (no GPU)
 int main(int argc, char **argv)
 {
   if(argc < 2)
     return 2;
+  if(argc >= 4 && std::strcmp(argv[2], "--scene") == 0)
+    return runSceneFile(argv[1], argv[3]);
   vMeshData mesh;
   const bool withMesh = argc >= 3;
   if(withMesh && !loadMesh(argv[2], mesh))

@@ -1,9 +1,11 @@
 """Multi-rank tile sharding on CPU: torch.distributed over gloo, world_size 2
-and 3.  Each rank renders only its 16-row bands (oracle on CPU, standing in
-for the per-GPU kernel), the bands are gathered to rank 0 with one
-collective per step exactly as bench.py / tiles.BandGather do over RCCL, and
-rank 0's reassembled image must equal the single-process render bit for bit
-(seeds depend only on global pixel coordinates, PathTracer.cu:817-818).
+and 3.  Each rank renders only its 16x16 tiles, dealt round-robin (tile t
+belongs to rank t % N; the oracle on CPU stands in for the per-GPU kernel),
+the packed tiles are gathered to rank 0 with one collective per step as
+bench.py / tiles.TileGather do (over RCCL on GPUs, through the library's
+vrhip_comm_gather), and rank 0's reassembled image must equal the
+single-process render bit for bit (seeds depend only on global pixel
+coordinates, PathTracer.cu:817-818).
 """
 import os
 import socket

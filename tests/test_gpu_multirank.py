@@ -27,17 +27,22 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, backend="gloo"):
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
     from vrenderer_pathtracer_amd import VRendererHIP, scenes
     from vrenderer_pathtracer_amd.tiles import WHAT_ACCUM, WHAT_RGBA8, TileGather
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device("cuda", 0)
+    gpu = rank if backend == "nccl" else 0          # RCCL: one rank per GPU
+    dev = torch.device("cuda", gpu)
+    torch.cuda.set_device(gpu)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     sc = scenes.make_scene("C2", 160, 112)
-    r = VRendererHIP(0)
+    r = VRendererHIP(gpu)
     scenes.load_into(r, sc)
     r.set_tiling(rank, world)
     g_rgba = TileGather(r, rank, world, dev, WHAT_RGBA8)
@@ -53,6 +58,31 @@ def _worker(rank, world, port, out_dir):
     r.cleanUp()
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_rccl_tile_gather_equals_single_rank(native):
+    """The measured configuration: one rank per GPU, the tile gather through the
+    library's own RCCL communicator (vrhip_comm_init / vrhip_comm_gather:
+    pack, ncclGather over xGMI, unpack on rank 0).  Rank 0's image must equal
+    the single-GPU render bit for bit.  Needs two GPUs (RCCL refuses two ranks
+    on one device); the one-GPU boxes run the gloo rehearsal below instead."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs: RCCL refuses two ranks on one device")
+    from vrenderer_pathtracer_amd import VRendererHIP, scenes
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_worker, args=(2, _free_port(), td, "nccl"), nprocs=2, join=True)
+        acc = np.load(os.path.join(td, "accum.npy"))
+        rgba = np.load(os.path.join(td, "rgba.npy"))
+    sc = scenes.make_scene("C2", 160, 112)
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    for step in range(2):
+        r.render(frames=2, times=[sc["time"] + 2 * step + k for k in range(2)])
+    ref_acc, ref_rgba = r.read_accum(), r.read_rgba8()
+    r.cleanUp()
+    assert np.array_equal(acc.view(np.uint32), ref_acc.view(np.uint32))
+    assert np.array_equal(rgba, ref_rgba)
 
 
 @pytest.mark.parametrize("world", [2, 3])

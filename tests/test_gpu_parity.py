@@ -18,7 +18,7 @@ from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math, selfte
 pytestmark = pytest.mark.gpu
 
 TOL_RMSE = 1e-3          # north_star: per-pixel RMSE < 1e-3 vs the reference at equal spp
-TOL_PIX_FRAC = 0.99
+TOL_PIX_FRAC = 0.995     # >= 99.5 % of pixels with max-channel |delta| <= 1e-3
 
 
 def gpu_render(scene, frames=2, times=None, tiling=None, strict=False, split=None):

@@ -130,9 +130,13 @@ struct Cnt {
     // instrumented production kernels (F_COUNT_EXEC) only
     // and its lane loads by width (16 / 12 / 8 / 4 B) at every global-load site
     uint32_t nodes_lds = 0, tri_loads = 0, mesh_hits = 0, nmap_hits = 0, ld128 = 0, ld96 = 0, ld64 = 0, ld32 = 0;
-#ifdef VR_PATH_TIMES
-    // diagnostic build: per-lane node visits, triangle tests and outer
-    // traversal iterations, recorded per path with its start and end time
+    // the path kernel's cost of the lane's current path (node visits), summed
+    // per sub-tile for the next launch's longest-first order (RenderParams::sub_cost)
+    uint32_t work = 0;
+#ifdef VR_PATH_COUNTS
+    // diagnostic build (with VR_PATH_TIMES): per-lane node visits, triangle
+    // tests and outer traversal iterations, recorded per path with its start
+    // and end time
     uint32_t d_nodes = 0, d_tris = 0, d_iters = 0;
 #endif
 };
@@ -296,7 +300,8 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     int* stk = L.stk;
     const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
     if (COUNT) cnt.nodes += 1u;
-#ifdef VR_PATH_TIMES
+    cnt.work++;
+#ifdef VR_PATH_COUNTS
     cnt.d_nodes++;
 #endif
     vr4 n0, n1, nz;
@@ -430,7 +435,7 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 {
     const bool strict = HAS(F_STRICT);
     if (COUNT) cnt.tris++;
-#ifdef VR_PATH_TIMES
+#ifdef VR_PATH_COUNTS
     cnt.d_tris++;
 #endif
     const vr4 v0 = mk4(t.a0.x, t.a0.y, t.a0.z, 0.f);
@@ -483,11 +488,29 @@ constexpr int node_break() {
     // 2,147 -> 2,103 Mpaths/s with 10 (r02h)
     return ((FEAT & F_EXACT) && (FEAT & F_CORNELL) && !(FEAT & F_INLINE_PRIM)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK;
 }
+// The node-loop exit is proportional to the lanes in the call: a full wave
+// leaves once at most node_break of its 64 lanes still search (throughput:
+// the rest of the wave need not wait for its slowest searches), a wave with
+// few traversing lanes -- the sparse waves of a launch's drain, or a wave
+// whose other lanes are shading -- waits for all of them, as the reference's
+// vote does (:353-363).  A fixed threshold made a sparse wave's lanes leave
+// after ONE node visit per outer iteration: the most expensive paths (C2:
+// ~200 node visits, ~100 triangle tests) then needed 50-150 outer iterations
+// and ran 300-770 us, the critical path of a one-frame launch (r03 drain
+// diagnostics, scripts/path_times.py).
+#ifndef VR_NODE_BREAK_PROP
+#define VR_NODE_BREAK_PROP 1
+#endif
 template <int STACK, bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
 {
-#ifdef VR_PATH_TIMES
+#ifdef VR_PATH_COUNTS
     cnt.d_iters++;
+#endif
+#if VR_NODE_BREAK_PROP
+    const int brk = node_break<FEAT>() * __popcll(__ballot(1));  // exit when searching * 64 <= brk
+#else
+    const int brk = node_break<FEAT>() * 64;
 #endif
     int leafAddr = 0;
     while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
@@ -498,7 +521,7 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         }
         // the wave moves on to the leaves once (nearly) every lane holds one;
         // lanes still searching resume in the next outer iteration
-        if (__popcll(__ballot(leafAddr >= 0)) <= node_break<FEAT>()) break;
+        if (__popcll(__ballot(leafAddr >= 0)) * 64 <= brk) break;
     }
     while (leafAddr < 0) {
         const int lv = ~leafAddr;
@@ -1182,6 +1205,26 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
 #define VR_SHADE_RATIO 1
 #endif
 enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3, LS_CAMERA = 4 };
+// Age-based wave priority (s_setprio) in the path kernel, thresholds in us:
+// VR_AGE_PRIO 1 in every path kernel, 2 in the one-frame kernels only
+// (F_INLINE_PRIM: the reference's render() cadence, where a launch ends on
+// its oldest paths), 0 off.  Measured (r03e, 1xMI355X): one frame per call
+// C2 0.840 -> 0.799 ms, C3 0.564 -> 0.570 (noise); 16-frame launches C2
+// -0.4 %, C3 -0.1 %.
+#ifndef VR_AGE_PRIO
+#define VR_AGE_PRIO 2
+#endif
+template <uint32_t FEAT>
+constexpr bool age_prio() { return VR_AGE_PRIO == 1 || (VR_AGE_PRIO == 2 && (FEAT & F_INLINE_PRIM) != 0u); }
+#ifndef VR_AGE_T1
+#define VR_AGE_T1 100
+#endif
+#ifndef VR_AGE_T2
+#define VR_AGE_T2 200
+#endif
+#ifndef VR_AGE_T3
+#define VR_AGE_T3 300
+#endif
 
 // Block size of the path kernel: its blocks hold no tiles, so one block of
 // 1,024 threads per CU shares one LDS node cache four times the size of a
@@ -1310,7 +1353,9 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             const uint32_t r = o / n_paths;
             const uint32_t sb = (g * 8u + x) * (uint32_t)VR_XCD_BANDS + r;
             if (sb < n_sub) {
-                sub = sb;
+                // longest-first: the XCD's sub-tiles in the order of the
+                // previous launch's cost (order_kernel); else band order
+                sub = p.sub_order ? p.sub_order[x * p.order_cap + g * (uint32_t)VR_XCD_BANDS + r] : sb;
                 path = o - r * n_paths;
                 return;
             }
@@ -1338,12 +1383,17 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     uint32_t cam_xy = 0;                                   // F_INLINE_PRIM: its pixel (x << 16 | y) until LS_CAMERA
 #ifdef VR_PATH_TIMES
     uint64_t pstart = 0;                                   // diagnostic: this lane's path start, primary hit kind
-    uint32_t pkind = 0, p0n = 0, p0t = 0, p0i = 0;        // and its counts at the start
+    uint32_t pkind = 0;
+#ifdef VR_PATH_COUNTS
+    uint32_t p0n = 0, p0t = 0, p0i = 0;                    // and its counts at the start
+#endif
 #endif
     Ray ray;
     PathState ps;
     HitRec hr;
     Trav tr;
+    uint32_t born = 0;                                     // age_prio: this lane's path start (s_memrealtime, 100 MHz)
+    uint32_t now_tick = age_prio<FEAT>() ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
         if (sub == ~0u) { state = LS_DONE; return; }
         q = path;
@@ -1355,10 +1405,14 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         uint32_t s2 = y * p.times[f];
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
         path_begin(ps, s1, s2);
+        born = now_tick;
+        cnt.work = 0;
 #ifdef VR_PATH_TIMES
         pstart = __builtin_amdgcn_s_memrealtime();
         pkind = 15u;
+#ifdef VR_PATH_COUNTS
         p0n = cnt.d_nodes; p0t = cnt.d_tris; p0i = cnt.d_iters;
+#endif
 #endif
         if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {      // few paths per pixel: trace the camera ray here
             cam_xy = (x << 16) | y;                        // (set up at the top of the loop, out of the refill)
@@ -1385,6 +1439,17 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     start(cur_sub, cur_q, (uint32_t)lane);
 
     for (;;) {
+        if constexpr (age_prio<FEAT>()) {
+            // age-based issue priority: a wave holding an old path issues
+            // ahead of the SIMD's other waves, so the longest paths -- the
+            // end of the launch -- are not also the slowest
+            now_tick = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            const uint32_t age = state != LS_DONE ? now_tick - born : 0u;
+            if (__ballot(age > (uint32_t)(VR_AGE_T3 * 100)) != 0ull) __builtin_amdgcn_s_setprio(3);
+            else if (__ballot(age > (uint32_t)(VR_AGE_T2 * 100)) != 0ull) __builtin_amdgcn_s_setprio(2);
+            else if (__ballot(age > (uint32_t)(VR_AGE_T1 * 100)) != 0ull) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {
             if (state == LS_CAMERA) {
                 ray = camera_ray(p, cam_xy >> 16, cam_xy & 0xffffu);
@@ -1425,6 +1490,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #endif
             if (bounce_step<CNT, FEAT>(p, ray, hr, ps, out, cnt)) {
                 store_path(p, q, slot, out, ps.depth);
+                if (p.sub_cost) atomicAdd(p.sub_cost + (slot >> 6), cnt.work);
 #ifdef VR_PATH_TIMES
                 const size_t pidx = (size_t)q * p.path_stride + slot;
                 if (p.counters && pidx < kPathTimesCap) {
@@ -1434,8 +1500,12 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                     unsigned long long* pr = p.counters + kWaveTimesBase + 3 * 8192 + 3 * pidx;
                     pr[0] = pstart;
                     pr[1] = __builtin_amdgcn_s_memrealtime() | ((unsigned long long)pkind << 56);
+#ifdef VR_PATH_COUNTS
                     auto c20 = [](uint32_t v) { return (unsigned long long)(v < 0xfffffu ? v : 0xfffffu); };
                     pr[2] = c20(cnt.d_nodes - p0n) | (c20(cnt.d_tris - p0t) << 20) | (c20(cnt.d_iters - p0i) << 40);
+#else
+                    pr[2] = 0ull;
+#endif
                 }
 #endif
                 ended = true;
@@ -1469,6 +1539,55 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     }
 #endif
     if (CNT) flush_counts(p, cnt, lane, true);
+}
+
+// Longest-first order of a launch's sub-tiles for the next launch on the
+// same scratch (RenderParams::sub_order): block x sorts the sub-tiles XCD x's
+// queues serve (bands of VR_XCD_BANDS, dealt round-robin to the 8 XCDs) by
+// the cost this launch measured (sub_cost: node visits of all their paths),
+// most expensive first, by a counting sort over half-octave cost classes, and
+// zeroes the costs for the next launch.  Scheduling only: any permutation
+// renders the same image (finish_kernel sums each pixel's paths in path order).
+constexpr int kCostClasses = 64;
+__device__ __forceinline__ uint32_t cost_class(uint32_t c)
+{
+    if (c < 2u) return c;
+    const uint32_t msb = 31u - (uint32_t)__builtin_clz(c);
+    return 2u * msb + ((c >> (msb - 1u)) & 1u);          // 0..63
+}
+__global__ void __launch_bounds__(1024) order_kernel(uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
+                                                      uint32_t n_sub, uint32_t cap)
+{
+    __shared__ uint32_t hist[kCostClasses];
+    const uint32_t x = blockIdx.x, tid = threadIdx.x;
+    constexpr uint32_t B = (uint32_t)VR_XCD_BANDS;
+    auto sub_of = [&](uint32_t k) { return ((k / B) * 8u + x) * B + (k % B); };
+    // this XCD's sub-tiles: k < n_x  <=>  sub_of(k) < n_sub
+    const uint32_t full = n_sub / (8u * B), rem = n_sub - full * 8u * B;
+    const uint32_t n_x = full * B + (rem > x * B ? (rem - x * B < B ? rem - x * B : B) : 0u);
+    if (tid < (uint32_t)kCostClasses) hist[tid] = 0u;
+    __syncthreads();
+    for (uint32_t k = tid; k < n_x; k += blockDim.x) atomicAdd(&hist[cost_class(cost[sub_of(k)])], 1u);
+    __syncthreads();
+    if (tid == 0) {                                      // start of each class, most expensive first
+        uint32_t acc = 0;
+        for (int c = kCostClasses - 1; c >= 0; --c) { const uint32_t h = hist[c]; hist[c] = acc; acc += h; }
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < n_x; k += blockDim.x) {
+        const uint32_t sb = sub_of(k);
+        const uint32_t pos = atomicAdd(&hist[cost_class(cost[sb])], 1u);
+        order[x * cap + pos] = sb;
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < n_x; k += blockDim.x) cost[sub_of(k)] = 0u;
+}
+
+int launch_order(uint32_t* cost, uint32_t* order, uint32_t n_sub, uint32_t cap, void* stream)
+{
+    if (n_sub == 0) return 0;
+    hipLaunchKernelGGL(order_kernel, dim3(8), dim3(1024), 0, (hipStream_t)stream, cost, order, n_sub, cap);
+    return (int)hipGetLastError();
 }
 
 __global__ void half_to_float_kernel(const uint16_t* __restrict__ src, vr4* __restrict__ dst, size_t n)
@@ -1542,14 +1661,18 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
     // one resident set: path_waves(STACK, C) waves per SIMD, 4 SIMDs per CU
     constexpr bool C = cornell_kernel<FEAT>();
     constexpr int BT = wave_block(STACK, C), BTS = wave_block_small(STACK, C);
+    // blocks per CU: the kernel's full residency, or fewer under a waves-per-SIMD cap
+    auto per_cu = [&](int bt) {
+        const uint32_t full = (uint32_t)path_blocks_per_cu(STACK, bt, C);
+        if (p.waves_cap == 0u) return full;
+        const uint32_t capped = p.waves_cap * 4u * 64u / (uint32_t)bt;
+        return capped < 1u ? 1u : (capped < full ? capped : full);
+    };
     if (BTS != BT && p.small_blocks) {
-        hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * path_blocks_per_cu(STACK, BTS, C)),
-                           dim3(BTS), 0, s, p);
+        hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * per_cu(BTS)), dim3(BTS), 0, s, p);
         return;
     }
-    constexpr uint32_t per_cu = (uint32_t)path_blocks_per_cu(STACK, BT, C);
-    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BT>), dim3(p.wave_blocks * per_cu),
-                       dim3(BT), 0, s, p);
+    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BT>), dim3(p.wave_blocks * per_cu(BT)), dim3(BT), 0, s, p);
 }
 
 // One scene specialisation, production (FEAT) or instrumented

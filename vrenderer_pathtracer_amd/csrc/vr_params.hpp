@@ -92,6 +92,14 @@ struct RenderParams {
     vr4* prim;                       // per owned pixel: the camera ray's closest hit (2 x vr4, primary_kernel)
     uint32_t* chunk_ctr;             // render_wave_kernel's work queue heads (zeroed by finish_kernel)
     uint32_t wave_blocks;            // render_wave_kernel: CUs to fill with one resident set of blocks
+    uint32_t waves_cap;              // render_wave_kernel: at most this many waves per SIMD (0: the kernel's residency)
+    // longest-first scheduling (render_wave_kernel): per sub-tile cost of this
+    // launch's paths (node visits; nullptr: not measured) and the order the
+    // previous launch on this scratch measured (per XCD, order_cap entries
+    // each; nullptr: band order)
+    uint32_t* sub_cost;
+    const uint32_t* sub_order;
+    uint32_t order_cap;
     uint32_t small_blocks;           // render_wave_kernel: 256-thread blocks (launches of < 2^24 paths)
     uint32_t n_queues;               // render_wave_kernel: work queue heads in use (VR_QUEUES / VR_QUEUES_LARGE)
     uint32_t inline_prim;            // paths trace their own camera ray (no primary_kernel pass; F_INLINE_PRIM kernel)
@@ -126,6 +134,8 @@ struct RenderParams {
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int count, void* stream);
 // use_scratch launches: sums the per-path results of launch_render in path order
 int launch_finish(const RenderParams& p, uint32_t n_tiles, void* stream);
+// sorts the sub-tiles of each XCD by the costs a launch measured (for the next launch) and zeroes them
+int launch_order(uint32_t* cost, uint32_t* order, uint32_t n_sub, uint32_t cap, void* stream);
 int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);
 int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,
                       uint32_t n_owned, uint32_t rank, uint32_t nranks, int unpack, void* stream);

@@ -101,12 +101,19 @@ struct vrhip_ctx {
         vr4* prim = nullptr;         // primary hits, 2 float4 per owned pixel
         size_t prim_cap = 0;         // float4 elements
         uint32_t* chunk_ctr = nullptr;   // wave kernel work queue heads
+        // longest-first scheduling: per sub-tile costs measured by the last
+        // launch on this scratch and the per-XCD order sorted from them
+        uint32_t* sub_cost = nullptr;
+        uint32_t* sub_order = nullptr;
+        size_t sub_cap = 0;          // sub-tiles the buffers hold
+        uint32_t order_nsub = 0;     // sub-tile count the order was sorted for (0: none)
         hipEvent_t done = nullptr;   // recorded on `s` after the render kernels
         hipEvent_t finished = nullptr;   // recorded on `stream` after the finish pass that read this scratch
         bool used = false;
     } lane[VR_PATH_STREAMS];
     uint32_t parity = 0;
     int overlap = -1;            // vrhip_set_overlap: 1 always, 0 never, -1 small launches only
+    bool cost_order = true;      // longest-first sub-tile order for small launches (VRHIP_COST_ORDER=0: off)
     bool join = true;            // the next launches must wait for everything queued on `stream`
     hipEvent_t ev_join = nullptr;
     // timing
@@ -458,6 +465,7 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     c->device = device;
     c->W = width; c->H = height;
     c->fov_scale = default_fov_scale();
+    if (const char* e = std::getenv("VRHIP_COST_ORDER")) c->cost_order = std::atoi(e) != 0;
     int rc;
     if ((rc = set_device(c)) != VRHIP_OK) { delete c; return rc; }
     auto cleanup = [&](int code) { vrhip_destroy(c); return code; };
@@ -518,7 +526,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->comm) (void)ncclCommDestroy(c->comm);
     dfree(c->comm_send); dfree(c->comm_recv);
     for (auto& l : c->lane) {
-        dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr);
+        dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr); dfree(l.sub_cost); dfree(l.sub_order);
         if (l.done) (void)hipEventDestroy(l.done);
         if (l.finished) (void)hipEventDestroy(l.finished);
         if (l.s) (void)hipStreamDestroy(l.s);
@@ -802,22 +810,36 @@ static int take_event(vrhip_ctx* c, hipEvent_t* e)
     return VRHIP_OK;
 }
 
-// Path groups per pixel for a launch of n_tiles tiles x k frames.  A thread
-// runs its pixel's paths back to back, so a launch needs enough (tile, group)
-// blocks to fill every CU several times over; otherwise the few heaviest
-// tiles (mesh-covered, long bounce chains) set the launch time.  Splitting
-// the 2k paths over more blocks costs one primary ray per group and a
-// 16 B/path result round trip through HBM.
+// Path groups per pixel for a sphere-only launch of n_tiles tiles x k frames
+// (mesh scenes use the path-pool kernel: no groups).  A thread runs its
+// pixel's paths back to back; with one group it accumulates them in registers
+// (no result scratch, no finish pass), so one group is the choice whenever
+// the launch has blocks enough to fill the GPU, and for one-frame launches
+// (2 paths per thread: little imbalance to hide).  Otherwise the paths are
+// split into the smallest power of two of groups that gives 16 blocks per CU
+// (four resident blocks per CU, four rounds).  Measured (1xMI355X, 16-frame
+// steps, scripts/split_sweep.py): C4 (8,040 tiles) split 1 0.634 ms, 2 0.638,
+// 4 0.639, 8 0.678; one frame per call 0.089 ms against 0.105-0.145; C1
+// (1,024 tiles) split 1 0.434, 2 0.319, 4 0.296, 8 0.299, 16 0.310; one frame
+// per call 0.062 (split 1) against 0.068.
 static uint32_t choose_split(const vrhip_ctx* c, uint32_t n_tiles, uint32_t k)
 {
     uint32_t t = c->path_split;
     if (t == 0) {
-        const uint32_t target = c->cu_count * 64u;    // blocks: 4 resident per CU x 16 rounds (measured, C2/C3)
+        const uint32_t target = c->cu_count * 16u;
         t = 1;
-        while (n_tiles * t < target && t < 2u * k) t *= 2;
+        if (k > 1)
+            while (n_tiles * t < target && t < 2u * k) t *= 2;
     }
     return std::max<uint32_t>(1u, std::min<uint32_t>(t, 2u * k));
 }
+
+// Entries per XCD in a longest-first order list: the most sub-tiles one XCD's
+// bands (VR_XCD_BANDS sub-tiles each, dealt round-robin to 8 XCDs) can hold.
+#ifndef VR_XCD_BANDS
+#define VR_XCD_BANDS 128
+#endif
+static size_t order_cap(size_t n_sub) { return (n_sub / (8u * VR_XCD_BANDS) + 1u) * VR_XCD_BANDS; }
 
 // Scratch of one path stream, allocated when the stream is first used and
 // grown when a launch needs more (growing waits for every reader first).
@@ -839,6 +861,17 @@ static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t p
         l.prim_cap = 0;
         HIP_TRY(hipMalloc((void**)&l.prim, prim_need * sizeof(vr4)));
         l.prim_cap = prim_need;
+    }
+    const size_t n_sub = path_stride / 64u;
+    if (n_sub > l.sub_cap) {                              // the order buffers hold 8 XCD lists of order_cap(n_sub)
+        dfree(l.sub_cost); dfree(l.sub_order);
+        l.sub_cap = 0; l.order_nsub = 0;
+        HIP_TRY(hipMalloc((void**)&l.sub_cost, n_sub * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc((void**)&l.sub_order, 8u * order_cap(n_sub) * sizeof(uint32_t)));
+        HIP_TRY(hipMemsetAsync(l.sub_cost, 0, n_sub * sizeof(uint32_t), c->stream));
+        HIP_TRY(hipEventRecord(c->ev_join, c->stream));
+        HIP_TRY(hipStreamWaitEvent(l.s, c->ev_join, 0));
+        l.sub_cap = n_sub;
     }
     if (!l.chunk_ctr) {
         const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * VR_MAX_QUEUES;
@@ -909,6 +942,12 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     // the path-pool kernel is persistent: one resident set of blocks per CU
     // (the launcher sizes it from the kernel's occupancy) draining the work queues
     p.wave_blocks = c->cu_count;
+    // VRHIP_WAVES_PER_SIMD: cap the path kernel's resident waves (experiments)
+    static const uint32_t env_waves = [] {
+        const char* e = std::getenv("VRHIP_WAVES_PER_SIMD");
+        return e ? (uint32_t)std::atoi(e) : 0u;
+    }();
+    p.waves_cap = env_waves;
     const bool wave_kernel = (f & vr::F_MESH) != 0u;   // mesh scenes: the path-pool kernel (scratch + finish pass)
     (void)hipGetLastError();            // launches below report their own errors only
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
@@ -969,6 +1008,14 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = reinterpret_cast<vr::vr3*>(l.paths); p.path_w = reinterpret_cast<float*>(p.paths + need);
             p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
+            // longest-first: launches whose drain is a large share of them (one
+            // frame per call, shards) measure per sub-tile costs and take their
+            // sub-tiles in the order the previous launch on this scratch measured
+            const uint32_t n_sub = p.path_stride / 64u;
+            const bool order = wave_kernel && small && count == 0 && c->cost_order;
+            p.sub_cost = order ? l.sub_cost : nullptr;
+            p.sub_order = (order && l.order_nsub == n_sub) ? l.sub_order : nullptr;
+            p.order_cap = (uint32_t)order_cap(n_sub);
             if (on_lane && l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
         }
         hipEvent_t k0 = nullptr, k1 = nullptr;
@@ -980,6 +1027,11 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         int e = vr::launch_render(p, n_tiles, stack, count, rs);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
         if (n_tiles) HIP_TRY(hipEventRecord(k1, rs));
+        if (p.sub_cost) {
+            e = vr::launch_order(p.sub_cost, l.sub_order, p.path_stride / 64u, p.order_cap, rs);
+            if (e != 0) return fail(VRHIP_ERR_HIP, std::string("order launch: ") + hipGetErrorString((hipError_t)e));
+            l.order_nsub = p.path_stride / 64u;
+        }
         if (on_lane) {
             HIP_TRY(hipEventRecord(l.done, rs));
             HIP_TRY(hipStreamWaitEvent(c->stream, l.done, 0));

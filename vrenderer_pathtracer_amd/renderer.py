@@ -80,6 +80,33 @@ def validate_flat(flat: dict) -> tuple[int, int]:
     return d.value, n.value
 
 
+_POWF_LUTS = {}
+
+
+def texture_to_float4(rgba8: np.ndarray, gamma: float, tex_type: int) -> np.ndarray:
+    """QImage pixels (uint8 (H,W,4), RGBA) -> the float4 texels
+    vRendererCuda::loadTexture uploads (src/vRendererCuda.cpp:344-368):
+    channel / 255.f; on DIFFUSE maps the colour channels raised to
+    1.f / gamma with std::pow(float, float) -- libm's powf, applied here
+    through a 256-entry table of its own results, so every texel rounds as
+    the C++ host's does (numpy's float32 power may differ by an ulp)."""
+    corr = np.float32(1.0) / np.float32(gamma) if gamma > 0.001 else np.float32(1.0)
+    lin = np.arange(256, dtype=np.float32) / np.float32(255.0)
+    if tex_type == DIFFUSE:
+        key = float(corr)
+        lut = _POWF_LUTS.get(key)
+        if lut is None:
+            libm = ctypes.CDLL("libm.so.6")
+            libm.powf.restype = ctypes.c_float
+            libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+            lut = np.array([libm.powf(float(v), key) for v in lin], np.float32)
+            _POWF_LUTS[key] = lut
+    else:
+        lut = lin
+    t = np.asarray(rgba8, np.uint8)
+    return np.stack([lut[t[..., 0]], lut[t[..., 1]], lut[t[..., 2]], lin[t[..., 3]]], -1).astype(np.float32)
+
+
 def load_merl(path: str) -> np.ndarray:
     """vBRDFLoader::loadBinary (src/BRDFLoader.cpp:15-50) through the C ABI:
     a MERL .binary file as float32[3*90*90*180] (planar R, G, B), ready for loadBRDF."""
@@ -217,11 +244,7 @@ class VRendererHIP:
         self._need_ctx()
         t = np.asarray(texture)
         if t.dtype == np.uint8:
-            c = np.float32(1.0 / gamma) if gamma > 0.001 else np.float32(1.0)
-            f = t.astype(np.float32) / np.float32(255.0)
-            if type == DIFFUSE:
-                f[..., :3] = np.power(f[..., :3], c, dtype=np.float32)
-            t = f
+            t = texture_to_float4(t, gamma, type)
         t = _f32(t)
         check(self._lib.vrhip_upload_texture(self._ctx, int(type), fptr(t), t.shape[1], t.shape[0]),
               "vrhip_upload_texture")
