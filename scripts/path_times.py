@@ -35,15 +35,16 @@ lib = _native.lib()
 npaths = r.owned_pixels() * 2 * F
 assert npaths <= 4 * 1024 * 1024, "the diagnostic build records at most 4M paths (kPathTimesCap)"
 NW = 8192
-nrec = NW + npaths            # records of 3 u64: per wave, then per path
+nrec = NW + (4 * npaths + 2) // 3   # in units of 3 u64: 3 per wave, then 4 per path
 buf = (ctypes.c_uint64 * (3 * nrec))()
+CLK = float(os.environ.get("PT_CLK_GHZ", "2.3"))   # effective shader clock (scripts/wave_times.py)
 KINDS = {0: "none", 1: "cornell", 2: "small", 3: "example", 4: "mesh", 15: "inline"}
 pc = np.percentile
 for rep in range(2):
     r.render(frames=F, times=[sc["time"] + rep * F + k for k in range(F)])
     r.sync()
     assert lib.vrhip_debug_wave_times(r._ctx, buf, nrec) == 0
-    a = np.frombuffer(buf, dtype=np.uint64)[3 * NW:3 * NW + 3 * npaths].reshape(npaths, 3)
+    a = np.frombuffer(buf, dtype=np.uint64)[3 * NW:3 * NW + 4 * npaths].reshape(npaths, 4)
     st = a[:, 0].astype(np.int64)
     en = (a[:, 1] & np.uint64((1 << 56) - 1)).astype(np.int64)
     kind = (a[:, 1] >> np.uint64(56)).astype(np.int64)
@@ -51,6 +52,9 @@ for rep in range(2):
     nodes = (a[:, 2] & m20).astype(np.int64)
     tris = ((a[:, 2] >> np.uint64(20)) & m20).astype(np.int64)
     iters = ((a[:, 2] >> np.uint64(40)) & m20).astype(np.int64)
+    m16 = np.uint64(0xffff)
+    # phase cycles (x16): trav_iter, help_step, own shading, others' shading -> us at CLK
+    ph = np.stack([((a[:, 3] >> np.uint64(16 * j)) & m16).astype(np.float64) * 16 / CLK / 1e3 for j in range(4)], 1)
     ok = st > 0
     t0 = st[ok].min()
     st = (st - t0) / 100.0
@@ -81,9 +85,16 @@ for rep in range(2):
               f"{pc(nodes[m], 50):.0f}  tris p50 {pc(tris[m], 50):.0f}  iters p50 {pc(iters[m], 50):.0f}  "
               f"us/iter p50 {pc(dur[m] / np.maximum(iters[m], 1), 50):.1f}")
     top = np.argsort(-np.where(ok, dur, -1))[:10]
-    print("  longest: start dur nodes tris iters kind")
+    print(f"  longest: start dur nodes tris iters kind | us in trav_iter help own-shade other-shade rest (at {CLK} GHz)")
     for i in top:
-        print(f"    {st[i]:6.0f} {dur[i]:6.0f} {nodes[i]:5d} {tris[i]:5d} {iters[i]:4d} {KINDS.get(int(kind[i]), kind[i])}")
+        rest = dur[i] - ph[i].sum()
+        print(f"    {st[i]:6.0f} {dur[i]:6.0f} {nodes[i]:5d} {tris[i]:5d} {iters[i]:4d} {KINDS.get(int(kind[i]), kind[i]):8s}"
+              f" | {ph[i, 0]:6.1f} {ph[i, 1]:6.1f} {ph[i, 2]:6.1f} {ph[i, 3]:6.1f} {rest:6.1f}")
+    for lab, m in (("ending in the last 100 us", late), ("all", ok)):
+        if m.sum():
+            mp = ph[m].mean(0)
+            print(f"  phases, mean over {lab}: dur {dur[m].mean():.1f} us = trav_iter {mp[0]:.1f} + help {mp[1]:.1f} + "
+                  f"own shade {mp[2]:.1f} + other shade {mp[3]:.1f} + rest {dur[m].mean() - mp.sum():.1f}")
     # correlation of duration with work
     w = nodes[ok] + 2 * tris[ok]
     print(f"  corr(dur, nodes+2*tris) {np.corrcoef(dur[ok], w)[0, 1]:.3f}  corr(dur, iters) "

@@ -41,7 +41,8 @@ def production(name):
     if "true" in args:
         return None
     feat = int(args[1].rstrip("u")) if m.group(1) != "render_kernel" else int(args[2].rstrip("u"))
-    return m.group(1) if feat >= 2 ** 31 else None
+    # exact scene specialisations (F_EXACT, bit 31), not the instrumented copies (F_COUNT_EXEC, bit 10)
+    return m.group(1) if feat >= 2 ** 31 and not (feat & (1 << 10)) else None
 
 
 def timed_durations(trace_csv):
@@ -122,8 +123,9 @@ def main():
                        "launch_ms_trace": launch_ms, "paths_per_launch": paths,
                        "source": f"profiles/{name}_summary.md ({os.path.basename(src.rstrip('/'))}, fetch_{cfg} / write_{cfg})",
                        "note": "2*FETCH_SIZE + WRITE_SIZE (KiB -> B) per render launch (production render kernels), "
-                               f"mean of the {STEPS} timed dispatches; FETCH doubling per MI355X_MICROARCH.md HBM "
-                               "(calibrated for wide streams; the kernel's reads are L2-resident gathers)"},
+                               f"mean of the {STEPS} timed dispatches; FETCH doubling per MI355X_MICROARCH.md HBM, "
+                               "checked for the kernel's 16/32/72-B gathers in profiles/r03_fetch_calibration.md "
+                               "(one 128-B line request per line touched, tallied at 64 B)"},
                       open(os.path.join(prof, f"traffic_{cfg.lower()}.json"), "w"), indent=1)
             md.append(f"\nHBM per launch: FETCH_SIZE {fetch / 1024:.1f} MiB, WRITE_SIZE {write / 1024:.1f} MiB -> "
                       f"2*FETCH + WRITE = {traffic / 1e6:.1f} MB = {traffic / 1e9 / (launch_ms / 1e3):.1f} GB/s "

@@ -9,6 +9,8 @@ Bar (DESIGN.md "Parity"):
     max-channel |delta| <= 1e-3 (libm ulp differences are amplified by
     branch flips in a few paths; SURVEY.md 8c measured that noise floor).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -532,3 +534,41 @@ def test_culled_vs_strict_full_frame(native, cfg, frames):
     n = int(diff.sum())
     print(f"{cfg}: {n} of {diff.size} pixels differ between culled and strict traversal")
     assert n / diff.size <= 1e-5
+
+
+@pytest.mark.parametrize("cfg,tiling,overlap", [("C3", None, 0), ("C2", (1, 3), -1), ("C5", (0, 2), 1)])
+def test_longest_first_order_is_scheduling_only(native, oracle, cfg, tiling, overlap):
+    """Small launches (one frame per call, shards) take their sub-tiles in the
+    order the previous launch on the same scratch measured (per-path costs
+    summed per sub-tile by the finish pass, sorted per XCD by order_kernel).
+    Consecutive one-frame calls -- the second and later ones ordered, on one
+    path stream or on three -- equal the band-order render bit for bit, and
+    the oracle."""
+    sc = scenes.make_scene(cfg, 160, 112) if cfg != "C5" else scenes.make_scene("C5", 96, 64, knot=(150, 75))
+    times = [sc["time"] + 7 * i for i in range(7)]
+    outs = []
+    for order in ("1", "0"):
+        old = os.environ.get("VRHIP_COST_ORDER")
+        os.environ["VRHIP_COST_ORDER"] = order
+        try:
+            r = VRendererHIP(0)
+        finally:
+            if old is None:
+                del os.environ["VRHIP_COST_ORDER"]
+            else:
+                os.environ["VRHIP_COST_ORDER"] = old
+        scenes.load_into(r, sc)
+        r.set_overlap(overlap)
+        if tiling:
+            r.set_tiling(*tiling)
+        for t in times:
+            r.render(frames=1, times=[t], sync=False)
+        r.sync()
+        outs.append((r.read_accum(), r.read_rgba8()))
+        r.cleanUp()
+    (acc1, rgba1), (acc0, rgba0) = outs
+    assert np.array_equal(acc1.view(np.uint32), acc0.view(np.uint32))
+    assert np.array_equal(rgba1, rgba0)
+    if tiling is None:
+        ref, _, _, _ = oracle.render(sc, frames=len(times), times=times, libm=oracle.LIBM_PORTABLE)
+        assert_bitexact(acc1, ref, sc, f"{cfg} ordered one-frame calls")

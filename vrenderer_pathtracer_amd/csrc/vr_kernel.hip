@@ -138,6 +138,10 @@ struct Cnt {
     // tests and outer traversal iterations, recorded per path with its start
     // and end time
     uint32_t d_nodes = 0, d_tris = 0, d_iters = 0;
+    // and the shader cycles the wave spent, while this lane's path was live,
+    // in trav_iter (lane traversing), help_step (lane traversing), shading
+    // (lane shading) and shading for other lanes (lane traversing or waiting)
+    uint32_t d_ct = 0, d_ch = 0, d_cs = 0, d_co = 0;
 #endif
 };
 
@@ -300,7 +304,7 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     int* stk = L.stk;
     const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
     if (COUNT) cnt.nodes += 1u;
-    cnt.work++;
+    if ((FEAT & F_SMALL) != 0u) cnt.work++;
 #ifdef VR_PATH_COUNTS
     cnt.d_nodes++;
 #endif
@@ -470,8 +474,8 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 
 // One outer iteration of the while-while loop: the inner node loop until
 // this lane holds a leaf and the wave agrees (ballot, :353-363), with one
-// leaf postponed (:345-351), then the leaf loop.  Precondition: tr.nodeAddr
-// is an inner node (not kSentinel).
+// leaf postponed (:345-351), then the leaf loop.  tr.nodeAddr is an inner
+// node, a leaf (a helper's first entry) or kSentinel (no-op).
 #ifndef VR_NODE_BREAK
 #define VR_NODE_BREAK 6    // measured (path kernel with paired triangle loads): 0 (the reference's
                            // all-lanes vote) C2 2,294, 2: 2,503, 4: 2,563, 6: 2,577, 8: 2,583 (C3 -2 %)
@@ -513,6 +517,10 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
     const int brk = node_break<FEAT>() * 64;
 #endif
     int leafAddr = 0;
+    if (tr.nodeAddr < 0) {                                      // a leaf to start with (a helper's subtree)
+        leafAddr = tr.nodeAddr;
+        tr.nodeAddr = trav_pop(tr, L);
+    }
     while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
         node_step<COUNT, FEAT>(p, r, tr, L, cnt);
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
@@ -1015,6 +1023,15 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     p.depth[ind] = dv;
     p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
     p.accum[ind] = io;
+    if (p.path_cost) {
+        // the sub-tile's cost for the next launch's order: its paths' costs,
+        // summed per pixel, then over the wave (one wave = one 8x8 sub-tile)
+        uint32_t c = 0;
+        for (uint32_t q = 0; q < n_paths; ++q) c += p.path_cost[(size_t)q * p.path_stride + slot];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+        if (lane == 0) p.sub_cost[tile * 4u + (uint32_t)wave] = c;
+    }
 }
 
 // Binds this thread's stack column and fills the block's node cache with
@@ -1204,7 +1221,109 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
 #ifndef VR_SHADE_RATIO
 #define VR_SHADE_RATIO 1
 #endif
-enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3, LS_CAMERA = 4 };
+// Once the queues are drained, the paths waiting to be shaded are shaded
+// together once n_shade * VR_DRAIN_SHADE_NUM >= n_trav * VR_DRAIN_SHADE_DEN
+// (or no lane traverses): each shading round costs the wave a whole pass
+// through the shading code, and in the drain the traversing lanes' paths --
+// the launch's longest -- wait through every such round.  Measured (r03o,
+// one frame per call; 8-rank shard steps): shading at the first waiting
+// path C3 0.504 / C2 0.765 ms, 0.631 / 1.333 ms; at n_shade >= n_trav 0.470 /
+// 0.731, 0.612 / 1.343; at 2 n_shade >= n_trav 0.476 / 0.740.
+#ifndef VR_DRAIN_SHADE_NUM
+#define VR_DRAIN_SHADE_NUM 1
+#endif
+#ifndef VR_DRAIN_SHADE_DEN
+#define VR_DRAIN_SHADE_DEN 1
+#endif
+enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3, LS_CAMERA = 4, LS_HELP = 5, LS_HELPDONE = 6 };
+
+// Helpers (the launch's drain).  Once the work queues are empty, a wave's
+// lanes idle as their paths end while a few lanes still walk long
+// traversals -- the paths that end the launch.  Then an idle lane takes the
+// top entry of a traversing lane's stack (a subtree or a leaf the owner
+// would visit next), walks it with the owner's ray, its closest hit so far
+// and its culling distance, and hands its closest hit back; the owner shades
+// once its own walk and all its helpers' are done.  The closest hit does not
+// depend on the order in which subtrees are visited: a triangle at exactly
+// the closest distance is resolved by the reference's own order (ref_first),
+// so the merged hit is the reference's.  Not used by the strict walk, whose
+// exact result relies on the reference's visit order.
+#ifndef VR_HELPERS
+#define VR_HELPERS 1
+#endif
+template <uint32_t FEAT>
+constexpr bool helpers() { return VR_HELPERS != 0 && (FEAT & F_STRICT) == 0u && (FEAT & F_SMALL) != 0u; }
+
+// One wave-synchronous help round: (1) finished helpers hand their closest
+// hit to their owners, one at a time; (2) idle lanes take a subtree each from
+// traversing lanes (one per owner per round, pairing the k-th idle lane with
+// the k-th owner).  For helpers `slot` holds the owner's lane.
+__device__ __forceinline__ uint32_t help_step(const RenderParams& p, int lane, int& state, int& pend, uint32_t& slot,
+                                              Ray& ray, Trav& tr, const Lds& L)
+{
+    unsigned long long hd = __ballot(state == LS_HELPDONE);
+    while (hd != 0ull) {
+        const int h = __ffsll((long long)hd) - 1;
+        hd &= hd - 1ull;
+        const int o = __builtin_amdgcn_readlane((int)slot, h);
+        const float ht = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tr.t), h));
+        const int hb = __builtin_amdgcn_readlane(tr.best, h);
+        const float hu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tr.bu), h));
+        const float hv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tr.bv), h));
+        if (lane == o) {
+            // the helper started from this lane's closest hit at the hand-out:
+            // it returns that one, a closer one, or a tie it resolved
+            const bool closer = hb >= 0 && (ht < tr.t || (ht == tr.t && hb != tr.best &&
+                                                          (tr.best < 0 || ref_first(p, tr, hb / 3, tr.best / 3))));
+            if (closer) {
+                tr.t = ht; tr.best = hb; tr.bu = hu; tr.bv = hv;
+                tr.tcull = tr.t * 1.0009765625f;
+            }
+            --pend;
+        }
+        if (lane == h) state = LS_DONE;
+    }
+    // helpers cull with the owner's closest hit as it improves
+    const int own = state == LS_HELP ? (int)slot : lane;
+    const float ot = __shfl(tr.t, own, 64);
+    if (state == LS_HELP) tr.tcull = __builtin_fminf(tr.tcull, ot * 1.0009765625f);
+    const bool idle = state == LS_DONE;
+    const bool can = state == LS_TRAV && tr.nodeAddr != kSentinel && tr.sp >= 1;
+    const unsigned long long im = __ballot(idle), cm = __ballot(can);
+    if (im == 0ull || cm == 0ull) return 0u;
+    const uint32_t ni = (uint32_t)__popcll(im), nc = (uint32_t)__popcll(cm), n = ni < nc ? ni : nc;
+    const uint32_t rc = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+    const uint32_t ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+    int give = 0;
+    if (can && rc < n) {                                   // the owner hands out its next stack entry
+        give = L.stk[tr.sp * L.stride];
+        tr.sp--;
+        ++pend;
+    }
+    int src = lane;                                        // idle lane ri takes the ri-th owner
+    unsigned long long m = cm;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int ol = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        if (idle && ri == k) src = ol;
+    }
+    const bool take = idle && ri < n;
+    const int e = __shfl(give, src, 64);
+    auto pull = [&](float& v) { v = __shfl(v, src, 64); };
+    pull(ray.o.x); pull(ray.o.y); pull(ray.o.z); pull(ray.o.w);
+    pull(ray.d.x); pull(ray.d.y); pull(ray.d.z); pull(ray.d.w);
+    pull(tr.ivx); pull(tr.ivy); pull(tr.ivz); pull(tr.odx); pull(tr.ody); pull(tr.odz);
+    pull(tr.t); pull(tr.tcull); pull(tr.bu); pull(tr.bv);
+    tr.best = __shfl(tr.best, src, 64);
+    if (take) {
+        state = LS_HELP;
+        slot = (uint32_t)src;
+        tr.sp = 0;
+        L.stk[0] = kSentinel;
+        tr.nodeAddr = e;
+    }
+    return n;                                              // subtrees handed out this round
+}
 // Age-based wave priority (s_setprio) in the path kernel, thresholds in us:
 // VR_AGE_PRIO 1 in every path kernel, 2 in the one-frame kernels only
 // (F_INLINE_PRIM: the reference's render() cadence, where a launch ends on
@@ -1219,12 +1338,25 @@ constexpr bool age_prio() { return VR_AGE_PRIO == 1 || (VR_AGE_PRIO == 2 && (FEA
 #ifndef VR_AGE_T1
 #define VR_AGE_T1 100
 #endif
+// Refill hold (small launches): a wave holding a path older than VR_HOLD_US
+// stops giving its ended lanes new paths until that path ends; its idle
+// lanes help the old path's traversal (as in the drain) and its rounds carry
+// fewer other paths' shading and setup.  The wave's chunk waits meanwhile.
+// 0: off.
+#ifndef VR_HOLD_US
+#define VR_HOLD_US 0
+#endif
+template <uint32_t FEAT>
+constexpr bool hold_old() { return VR_HOLD_US != 0 && (FEAT & F_SMALL) != 0u && (FEAT & F_STRICT) == 0u; }
+template <uint32_t FEAT>
+constexpr bool track_age() { return age_prio<FEAT>() || hold_old<FEAT>(); }
 #ifndef VR_AGE_T2
 #define VR_AGE_T2 200
 #endif
 #ifndef VR_AGE_T3
 #define VR_AGE_T3 300
 #endif
+
 
 // Block size of the path kernel: its blocks hold no tiles, so one block of
 // 1,024 threads per CU shares one LDS node cache four times the size of a
@@ -1277,11 +1409,18 @@ constexpr int path_cache_nodes(int stack, int bt, bool c) {
     return (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * 4) / 56 > 0
                ? (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * 4) / 56 : 1;
 }
+// small launches' Cornell kernels (shards) keep 6 waves: 7 waves (72 VGPRs)
+// spilled 19 VGPRs with helper lanes and cost counting; 8-rank C2 shard step
+// 1.317 -> 1.257 ms at 6 (r03p)
+#ifndef VR_SMALL_CORNELL7
+#define VR_SMALL_CORNELL7 0
+#endif
 template <uint32_t FEAT>
 constexpr bool cornell_kernel() {
     // the one-frame kernels (F_INLINE_PRIM) keep 6 waves: at 7 the interactive
     // C2 rate fell 2,147 -> 2,100 Mpaths/s (r02g)
-    return (FEAT & F_EXACT) != 0u && (FEAT & F_CORNELL) != 0u && (FEAT & F_INLINE_PRIM) == 0u;
+    return (FEAT & F_EXACT) != 0u && (FEAT & F_CORNELL) != 0u && (FEAT & F_INLINE_PRIM) == 0u &&
+           (VR_SMALL_CORNELL7 != 0 || (FEAT & F_SMALL) == 0u);
 }
 
 #ifndef VR_XCD_BANDS
@@ -1373,7 +1512,8 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     };
 #ifdef VR_WAVE_TIMES
     const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t wpaths = 0;
+    const uint64_t wc0 = __builtin_amdgcn_s_memtime();     // shader clock: the wave's effective clock
+    uint32_t wpaths = 0, wsteals = 0;
 #endif
     uint32_t cur_sub, cur_q;
     grab(cur_sub, cur_q);                                  // wave-uniform: chunk being handed out
@@ -1392,8 +1532,10 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     PathState ps;
     HitRec hr;
     Trav tr;
+    int pend = 0;                                          // helpers: subtrees this lane's walk handed out, not yet merged
     uint32_t born = 0;                                     // age_prio: this lane's path start (s_memrealtime, 100 MHz)
-    uint32_t now_tick = age_prio<FEAT>() ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+    uint32_t now_tick = track_age<FEAT>() ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+    bool hold = false;                                     // hold_old: no refills this round
     auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
         if (sub == ~0u) { state = LS_DONE; return; }
         q = path;
@@ -1406,12 +1548,13 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
         path_begin(ps, s1, s2);
         born = now_tick;
-        cnt.work = 0;
+        if constexpr ((FEAT & F_SMALL) != 0u) cnt.work = 0;
 #ifdef VR_PATH_TIMES
         pstart = __builtin_amdgcn_s_memrealtime();
         pkind = 15u;
 #ifdef VR_PATH_COUNTS
         p0n = cnt.d_nodes; p0t = cnt.d_tris; p0i = cnt.d_iters;
+        cnt.d_ct = cnt.d_ch = cnt.d_cs = cnt.d_co = 0;
 #endif
 #endif
         if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {      // few paths per pixel: trace the camera ray here
@@ -1439,11 +1582,15 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     start(cur_sub, cur_q, (uint32_t)lane);
 
     for (;;) {
+        if constexpr (track_age<FEAT>()) now_tick = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        if constexpr (hold_old<FEAT>()) {
+            const bool live = state == LS_SETUP || state == LS_TRAV || state == LS_SHADE || state == LS_CAMERA;
+            hold = cur_sub != ~0u && __ballot(live && now_tick - born > (uint32_t)(VR_HOLD_US * 100)) != 0ull;
+        }
         if constexpr (age_prio<FEAT>()) {
             // age-based issue priority: a wave holding an old path issues
             // ahead of the SIMD's other waves, so the longest paths -- the
             // end of the launch -- are not also the slowest
-            now_tick = (uint32_t)__builtin_amdgcn_s_memrealtime();
             const uint32_t age = state != LS_DONE ? now_tick - born : 0u;
             if (__ballot(age > (uint32_t)(VR_AGE_T3 * 100)) != 0ull) __builtin_amdgcn_s_setprio(3);
             else if (__ballot(age > (uint32_t)(VR_AGE_T2 * 100)) != 0ull) __builtin_amdgcn_s_setprio(2);
@@ -1466,23 +1613,53 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         }
         if (HAS(F_MESH)) {
             for (;;) {
-                const int n_trav = __popcll(__ballot(state == LS_TRAV));
+                const int n_trav = __popcll(__ballot(state == LS_TRAV || state == LS_HELP));
                 if (n_trav == 0) break;
                 const int n_shade = __popcll(__ballot(state == LS_SHADE));
                 if (n_shade >= VR_SHADE_BATCH && n_shade * VR_SHADE_RATIO >= n_trav) break;
-                // queue drained: no lane will be refilled, so a path waiting to
-                // be shaded is only delayed by the others' traversal
-                if (cur_sub == ~0u && n_shade > 0) break;
-                if (state == LS_TRAV) {
-                    trav_iter<STACK, CNT, FEAT>(p, ray, tr, L, cnt);
-                    if (tr.nodeAddr == kSentinel) {
-                        trav_finish(tr, hr);
-                        state = LS_SHADE;
+                // queue drained: no lane will be refilled; shade in batches
+                if ((cur_sub == ~0u || hold) && n_shade > 0 && n_shade * VR_DRAIN_SHADE_NUM >= n_trav * VR_DRAIN_SHADE_DEN)
+                    break;
+#ifdef VR_PATH_COUNTS
+                const uint64_t c0 = __builtin_amdgcn_s_memtime();
+                const bool own_trav = state == LS_TRAV;
+#endif
+                if constexpr (helpers<FEAT>()) {
+                    // (and until helpers a hold started are merged, after it ends)
+                    if (cur_sub == ~0u || hold || __ballot(state == LS_HELP || state == LS_HELPDONE) != 0ull) {
+                        const uint32_t given = help_step(p, lane, state, pend, slot, ray, tr, L);
+#ifdef VR_WAVE_TIMES
+                        wsteals += given;
+#else
+                        (void)given;
+#endif
                     }
                 }
+#ifdef VR_PATH_COUNTS
+                const uint64_t c1 = __builtin_amdgcn_s_memtime();
+                if (own_trav) cnt.d_ch += (uint32_t)(c1 - c0);
+#endif
+                if (state == LS_TRAV || state == LS_HELP) {
+                    trav_iter<STACK, CNT, FEAT>(p, ray, tr, L, cnt);
+                    if (tr.nodeAddr == kSentinel) {
+                        if (state == LS_HELP) {
+                            state = LS_HELPDONE;           // its best hit waits for the owner (help_step)
+                        } else if (pend == 0) {
+                            trav_finish(tr, hr);
+                            state = LS_SHADE;
+                        }                                  // else: the owner waits for its helpers
+                    }
+                }
+#ifdef VR_PATH_COUNTS
+                if (own_trav) cnt.d_ct += (uint32_t)(__builtin_amdgcn_s_memtime() - c1);
+#endif
             }
         }
         bool ended = false;
+#ifdef VR_PATH_COUNTS
+        const uint64_t cs0 = __builtin_amdgcn_s_memtime();
+        const bool own_shade = state == LS_SHADE, live = state == LS_TRAV || state == LS_HELP || state == LS_SHADE;
+#endif
         if (state == LS_SHADE) {
             vr4 out;
 #ifdef VR_PATH_TIMES
@@ -1490,21 +1667,29 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #endif
             if (bounce_step<CNT, FEAT>(p, ray, hr, ps, out, cnt)) {
                 store_path(p, q, slot, out, ps.depth);
-                if (p.sub_cost) atomicAdd(p.sub_cost + (slot >> 6), cnt.work);
+                if constexpr ((FEAT & F_SMALL) != 0u) {
+                    if (p.path_cost)
+                        p.path_cost[(size_t)q * p.path_stride + slot] = (uint8_t)(cnt.work < 510u ? cnt.work >> 1 : 255u);
+                }
 #ifdef VR_PATH_TIMES
                 const size_t pidx = (size_t)q * p.path_stride + slot;
                 if (p.counters && pidx < kPathTimesCap) {
-                    // diagnostic: start, end | primary hit kind << 56, and the
+                    // diagnostic: start, end | primary hit kind << 56, the
                     // path's node visits | triangle tests << 20 | outer
-                    // traversal iterations << 40 (20 bits each)
-                    unsigned long long* pr = p.counters + kWaveTimesBase + 3 * 8192 + 3 * pidx;
+                    // traversal iterations << 40 (20 bits each), and its
+                    // phase cycles / 16 (Cnt::d_ct, d_ch, d_cs, d_co; 16 bits each)
+                    unsigned long long* pr = p.counters + kWaveTimesBase + 3 * 8192 + kPathRec * pidx;
                     pr[0] = pstart;
                     pr[1] = __builtin_amdgcn_s_memrealtime() | ((unsigned long long)pkind << 56);
 #ifdef VR_PATH_COUNTS
+                    cnt.d_cs += (uint32_t)(__builtin_amdgcn_s_memtime() - cs0);
                     auto c20 = [](uint32_t v) { return (unsigned long long)(v < 0xfffffu ? v : 0xfffffu); };
+                    auto c16 = [](uint32_t v) { v >>= 4; return (unsigned long long)(v < 0xffffu ? v : 0xffffu); };
                     pr[2] = c20(cnt.d_nodes - p0n) | (c20(cnt.d_tris - p0t) << 20) | (c20(cnt.d_iters - p0i) << 40);
+                    pr[3] = c16(cnt.d_ct) | (c16(cnt.d_ch) << 16) | (c16(cnt.d_cs) << 32) | (c16(cnt.d_co) << 48);
 #else
                     pr[2] = 0ull;
+                    pr[3] = 0ull;
 #endif
                 }
 #endif
@@ -1512,6 +1697,19 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             } else {
                 state = LS_SETUP;
             }
+        }
+#ifdef VR_PATH_COUNTS
+        {
+            const uint32_t dc = (uint32_t)(__builtin_amdgcn_s_memtime() - cs0);
+            if (own_shade && !ended) cnt.d_cs += dc;
+            else if (live && !own_shade) cnt.d_co += dc;
+        }
+#endif
+        if constexpr (hold_old<FEAT>()) {
+            // held: ended lanes idle (LS_DONE) until the old path ends; then
+            // every idle lane is refilled
+            if (hold && ended) { state = LS_DONE; ended = false; }
+            else if (!hold && cur_sub != ~0u && state == LS_DONE) ended = true;
         }
         const unsigned long long em = __ballot(ended);
         if (em != 0ull) {
@@ -1535,7 +1733,9 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #ifdef VR_WAVE_TIMES
     if (p.counters && lane == 0) {   // diagnostic: per-wave start / end (100 MHz) and paths completed
         unsigned long long* w = p.counters + kWaveTimesBase + 3 * (blockIdx.x * (uint32_t)(BT / 64) + (uint32_t)(tid >> 6));
-        w[0] = wt0; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = wpaths;
+        const uint64_t wc1 = __builtin_amdgcn_s_memtime();
+        w[0] = wt0; w[1] = __builtin_amdgcn_s_memrealtime();
+        w[2] = (uint64_t)(wpaths & 0xffffu) | ((uint64_t)(wsteals & 0xffffu) << 16) | ((wc1 - wc0) << 32);
     }
 #endif
     if (CNT) flush_counts(p, cnt, lane, true);
@@ -1544,10 +1744,10 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 // Longest-first order of a launch's sub-tiles for the next launch on the
 // same scratch (RenderParams::sub_order): block x sorts the sub-tiles XCD x's
 // queues serve (bands of VR_XCD_BANDS, dealt round-robin to the 8 XCDs) by
-// the cost this launch measured (sub_cost: node visits of all their paths),
-// most expensive first, by a counting sort over half-octave cost classes, and
-// zeroes the costs for the next launch.  Scheduling only: any permutation
-// renders the same image (finish_kernel sums each pixel's paths in path order).
+// the cost this launch measured (sub_cost, written by finish_kernel: node
+// visits of all their paths), most expensive first, by a counting sort over
+// half-octave cost classes.  Scheduling only: any permutation renders the
+// same image (finish_kernel sums each pixel's paths in path order).
 constexpr int kCostClasses = 64;
 __device__ __forceinline__ uint32_t cost_class(uint32_t c)
 {
@@ -1555,7 +1755,7 @@ __device__ __forceinline__ uint32_t cost_class(uint32_t c)
     const uint32_t msb = 31u - (uint32_t)__builtin_clz(c);
     return 2u * msb + ((c >> (msb - 1u)) & 1u);          // 0..63
 }
-__global__ void __launch_bounds__(1024) order_kernel(uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
+__global__ void __launch_bounds__(1024) order_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
                                                       uint32_t n_sub, uint32_t cap)
 {
     __shared__ uint32_t hist[kCostClasses];
@@ -1579,8 +1779,6 @@ __global__ void __launch_bounds__(1024) order_kernel(uint32_t* __restrict__ cost
         const uint32_t pos = atomicAdd(&hist[cost_class(cost[sb])], 1u);
         order[x * cap + pos] = sb;
     }
-    __syncthreads();
-    for (uint32_t k = tid; k < n_x; k += blockDim.x) cost[sub_of(k)] = 0u;
 }
 
 int launch_order(uint32_t* cost, uint32_t* order, uint32_t n_sub, uint32_t cap, void* stream)
@@ -1656,11 +1854,17 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
     if constexpr ((FEAT & (F_INLINE_PRIM | F_COUNT_EXEC)) == 0u) {
         if (p.inline_prim) { launch_wave<STACK, FEAT | F_INLINE_PRIM>(p, n_tiles, s); return; }
     }
+    if constexpr ((FEAT & (F_SMALL | F_COUNT_EXEC)) == 0u) {
+        if (p.small_blocks) { launch_wave<STACK, FEAT | F_SMALL>(p, n_tiles, s); return; }
+    }
     if constexpr ((FEAT & F_INLINE_PRIM) == 0u)
-        hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
-    // one resident set: path_waves(STACK, C) waves per SIMD, 4 SIMDs per CU
+        hipLaunchKernelGGL((primary_kernel<STACK, FEAT & ~F_SMALL>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    // one resident set: path_waves(STACK, C) waves per SIMD, 4 SIMDs per CU;
+    // small launches (and the instrumented copy of one) in the smaller blocks
     constexpr bool C = cornell_kernel<FEAT>();
-    constexpr int BT = wave_block(STACK, C), BTS = wave_block_small(STACK, C);
+    constexpr int BT = ((FEAT & F_SMALL) != 0u) ? wave_block_small(STACK, C) : wave_block(STACK, C);
+    constexpr int BTS = wave_block_small(STACK, C);
+    constexpr int B = ((FEAT & F_COUNT_EXEC) != 0u && BTS != BT) ? 0 : BT;   // counted: picked at run time below
     // blocks per CU: the kernel's full residency, or fewer under a waves-per-SIMD cap
     auto per_cu = [&](int bt) {
         const uint32_t full = (uint32_t)path_blocks_per_cu(STACK, bt, C);
@@ -1668,9 +1872,11 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
         const uint32_t capped = p.waves_cap * 4u * 64u / (uint32_t)bt;
         return capped < 1u ? 1u : (capped < full ? capped : full);
     };
-    if (BTS != BT && p.small_blocks) {
-        hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * per_cu(BTS)), dim3(BTS), 0, s, p);
-        return;
+    if constexpr (B == 0) {
+        if (p.small_blocks) {
+            hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * per_cu(BTS)), dim3(BTS), 0, s, p);
+            return;
+        }
     }
     hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BT>), dim3(p.wave_blocks * per_cu(BT)), dim3(BT), 0, s, p);
 }

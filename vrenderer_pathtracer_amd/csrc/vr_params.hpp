@@ -31,6 +31,12 @@ enum Flags : uint32_t {
     // (paths trace their own camera ray; a separate instantiation, so the
     // multi-frame kernels keep the registers that code would take)
     F_INLINE_PRIM = 1u << 13,
+    // compile-time only: the path kernel of small launches (< 2^24 paths:
+    // one frame per call, shards), whose drain is a large share of the
+    // launch: it measures per-path costs for the next launch's longest-first
+    // order and lets idle lanes help the last traversals (vr_kernel.hip);
+    // a separate instantiation, so the whole-frame kernels keep those registers
+    F_SMALL = 1u << 14,
 };
 constexpr int kMaxFramesPerLaunch = 64;
 
@@ -46,6 +52,7 @@ constexpr int kExecCounterBase = 16;
 constexpr int kExecCounters = 8;
 constexpr int kWaveTimesBase = 32;   // -DVR_WAVE_TIMES diagnostic builds: per-wave records from here
 constexpr size_t kPathTimesCap = 4u * 1024u * 1024u;   // -DVR_PATH_TIMES: per-path records after them (paths of a launch)
+constexpr size_t kPathRec = 4;                          // u64 per path record
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
 // render_wave_kernel work queues: RenderParams::n_queues counters (a power of
@@ -93,10 +100,12 @@ struct RenderParams {
     uint32_t* chunk_ctr;             // render_wave_kernel's work queue heads (zeroed by finish_kernel)
     uint32_t wave_blocks;            // render_wave_kernel: CUs to fill with one resident set of blocks
     uint32_t waves_cap;              // render_wave_kernel: at most this many waves per SIMD (0: the kernel's residency)
-    // longest-first scheduling (render_wave_kernel): per sub-tile cost of this
-    // launch's paths (node visits; nullptr: not measured) and the order the
-    // previous launch on this scratch measured (per XCD, order_cap entries
-    // each; nullptr: band order)
+    // longest-first scheduling (render_wave_kernel): each path's cost (node
+    // visits / 2, saturated to a byte; same indexing as `paths`; nullptr: not
+    // measured), summed per sub-tile by finish_kernel into sub_cost, and the
+    // order the previous launch on this scratch measured (per XCD, order_cap
+    // entries each; nullptr: band order)
+    uint8_t* path_cost;
     uint32_t* sub_cost;
     const uint32_t* sub_order;
     uint32_t order_cap;
@@ -134,7 +143,7 @@ struct RenderParams {
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int count, void* stream);
 // use_scratch launches: sums the per-path results of launch_render in path order
 int launch_finish(const RenderParams& p, uint32_t n_tiles, void* stream);
-// sorts the sub-tiles of each XCD by the costs a launch measured (for the next launch) and zeroes them
+// sorts the sub-tiles of each XCD by the costs a launch measured (for the next launch on the same scratch)
 int launch_order(uint32_t* cost, uint32_t* order, uint32_t n_sub, uint32_t cap, void* stream);
 int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);
 int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,

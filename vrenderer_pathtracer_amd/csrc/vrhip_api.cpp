@@ -746,7 +746,7 @@ int vrhip_gl_present(vrhip_ctx* c)
 }
 
 #if defined(VR_WAVE_TIMES) && defined(VR_PATH_TIMES)
-constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192 + 3 * (int)vr::kPathTimesCap;   // + 3 per path
+constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192 + (int)(vr::kPathRec * vr::kPathTimesCap);   // + kPathRec per path
 #elif defined(VR_WAVE_TIMES)
 constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192;   // + per-wave start / end / paths of render_wave_kernel
 #else
@@ -868,15 +868,13 @@ static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t p
         l.sub_cap = 0; l.order_nsub = 0;
         HIP_TRY(hipMalloc((void**)&l.sub_cost, n_sub * sizeof(uint32_t)));
         HIP_TRY(hipMalloc((void**)&l.sub_order, 8u * order_cap(n_sub) * sizeof(uint32_t)));
-        HIP_TRY(hipMemsetAsync(l.sub_cost, 0, n_sub * sizeof(uint32_t), c->stream));
-        HIP_TRY(hipEventRecord(c->ev_join, c->stream));
-        HIP_TRY(hipStreamWaitEvent(l.s, c->ev_join, 0));
         l.sub_cap = n_sub;
     }
     if (!l.chunk_ctr) {
         const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * VR_MAX_QUEUES;
         HIP_TRY(hipMalloc((void**)&l.chunk_ctr, bytes));
         HIP_TRY(hipMemsetAsync(l.chunk_ctr, 0, bytes, c->stream));
+
         HIP_TRY(hipEventRecord(c->ev_join, c->stream));
         HIP_TRY(hipStreamWaitEvent(l.s, c->ev_join, 0));
     }
@@ -1013,6 +1011,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             // sub-tiles in the order the previous launch on this scratch measured
             const uint32_t n_sub = p.path_stride / 64u;
             const bool order = wave_kernel && small && count == 0 && c->cost_order;
+            // per-path costs after the radiances and depth terms in the scratch
+            // (need x 16 B holds need x 12 + path_stride x 4 + need x 1)
+            p.path_cost = order ? reinterpret_cast<uint8_t*>(p.path_w + p.path_stride) : nullptr;
             p.sub_cost = order ? l.sub_cost : nullptr;
             p.sub_order = (order && l.order_nsub == n_sub) ? l.sub_order : nullptr;
             p.order_cap = (uint32_t)order_cap(n_sub);
@@ -1027,17 +1028,17 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         int e = vr::launch_render(p, n_tiles, stack, count, rs);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
         if (n_tiles) HIP_TRY(hipEventRecord(k1, rs));
-        if (p.sub_cost) {
-            e = vr::launch_order(p.sub_cost, l.sub_order, p.path_stride / 64u, p.order_cap, rs);
-            if (e != 0) return fail(VRHIP_ERR_HIP, std::string("order launch: ") + hipGetErrorString((hipError_t)e));
-            l.order_nsub = p.path_stride / 64u;
-        }
         if (on_lane) {
             HIP_TRY(hipEventRecord(l.done, rs));
             HIP_TRY(hipStreamWaitEvent(c->stream, l.done, 0));
         }
         e = vr::launch_finish(p, n_tiles, c->stream);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("finish launch: ") + hipGetErrorString((hipError_t)e));
+        if (p.path_cost) {           // the next launch on this scratch takes this launch's order
+            e = vr::launch_order(p.sub_cost, l.sub_order, p.path_stride / 64u, p.order_cap, c->stream);
+            if (e != 0) return fail(VRHIP_ERR_HIP, std::string("order launch: ") + hipGetErrorString((hipError_t)e));
+            l.order_nsub = p.path_stride / 64u;
+        }
         if (p.use_scratch) {
             HIP_TRY(hipEventRecord(l.finished, c->stream));
             l.used = true;
