@@ -143,6 +143,12 @@ struct Cnt {
     // (lane shading) and shading for other lanes (lane traversing or waiting)
     uint32_t d_ct = 0, d_ch = 0, d_cs = 0, d_co = 0;
 #endif
+#ifdef VR_WAVE_PHASES
+    uint32_t w_steps = 0, w_pairs = 0;   // diagnostic: node-loop and leaf-pair rounds this lane ran
+    // wave-level rounds of the node and leaf loops and their cycles, counted
+    // by the wave's lowest active lane (summed over the wave at its end)
+    uint32_t w_nr = 0, w_lr = 0, w_nc = 0, w_lc = 0;
+#endif
 };
 
 // Counting launches (COUNT) come in two kinds: the reference algorithm's
@@ -521,7 +527,14 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         leafAddr = tr.nodeAddr;
         tr.nodeAddr = trav_pop(tr, L);
     }
+#ifdef VR_WAVE_PHASES
+    const uint32_t wt0 = (uint32_t)__builtin_amdgcn_s_memtime();
+#endif
     while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
+#ifdef VR_WAVE_PHASES
+        cnt.w_steps++;
+        if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) cnt.w_nr++;
+#endif
         node_step<COUNT, FEAT>(p, r, tr, L, cnt);
         if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
             leafAddr = tr.nodeAddr;
@@ -531,6 +544,10 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         // lanes still searching resume in the next outer iteration
         if (__popcll(__ballot(leafAddr >= 0)) * 64 <= brk) break;
     }
+#ifdef VR_WAVE_PHASES
+    const uint32_t wt1 = (uint32_t)__builtin_amdgcn_s_memtime();
+    if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) cnt.w_nc += wt1 - wt0;
+#endif
     while (leafAddr < 0) {
         const int lv = ~leafAddr;
         const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
@@ -541,6 +558,10 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         // returns zeros (never tested)
         for (int k = lv >> kLeafCountBits; k < kend; k += 2) {
             const bool two = k + 1 < kend;
+#ifdef VR_WAVE_PHASES
+            cnt.w_pairs++;
+            if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) cnt.w_lr++;
+#endif
             TriV ta, tb;
             {
                 const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, p.n_tris * 36u);
@@ -563,6 +584,9 @@ __device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, T
         leafAddr = tr.nodeAddr;
         if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop(tr, L);
     }
+#ifdef VR_WAVE_PHASES
+    if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) cnt.w_lc += (uint32_t)__builtin_amdgcn_s_memtime() - wt1;
+#endif
 }
 
 __device__ __forceinline__ void trav_finish(const Trav& tr, HitRec& hr)
@@ -997,7 +1021,8 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
 {
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
     // the path kernel's queue heads, for the next launch on this scratch
-    if (tile == 0 && tid < VR_MAX_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride] = 0u;
+    if (tile == 0 && tid <= VR_MAX_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride] = 0u;
+    if (tile == 0 && tid == VR_MAX_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride + 1u] = 0u;   // drained-queue mask
     const int wave = (int)tid >> 6, lane = (int)tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
     const uint32_t tile_y = gtile / p.tiles_x;
@@ -1442,6 +1467,42 @@ __device__ __forceinline__ void sub_pixel(const RenderParams& p, uint32_t sub, u
     y = tile_y * 16u + (quad >> 1) * 8u + (px >> 3);
 }
 
+// The launch's drained-queue mask (bit q: head q has handed out its last
+// chunk), after the VR_MAX_QUEUES heads; reset with them by finish_kernel.
+__device__ __forceinline__ unsigned long long* queue_drained_mask(uint32_t* chunk_ctr)
+{
+    return reinterpret_cast<unsigned long long*>(chunk_ctr + VR_MAX_QUEUES * kQueueStride);
+}
+__device__ __forceinline__ unsigned long long all_q_of(uint32_t Q) { return Q >= 64u ? ~0ull : ((1ull << Q) - 1ull); }
+#ifndef VR_QSCAN
+#define VR_QSCAN 0
+#endif
+
+// The sub-tile that value v of work-queue head q hands out (>= n_sub: the
+// queue is drained; non-decreasing in v), and the path in `path`.
+// Chunk = (sub-tile, path): the paths of one sub-tile are handed out
+// together.  With VR_XCD_BANDS queue q serves XCD q % 8 (blocks b % 16 == q
+// under round-robin dispatch): bands of VR_XCD_BANDS sub-tiles are dealt
+// round-robin to the XCDs, each XCD's chunks sub-major, alternated between
+// its Q / 8 queues.
+__device__ __forceinline__ uint32_t queue_item(uint32_t q, uint32_t v, uint32_t Q, uint32_t n_paths, uint32_t& path)
+{
+#if VR_XCD_BANDS
+    const uint32_t x = q % 8u, h = q / 8u;
+    const uint32_t e = v * (Q / 8u) + h;
+    const uint32_t per_band = (uint32_t)VR_XCD_BANDS * n_paths;
+    const uint32_t g = e / per_band, o = e - g * per_band;
+    const uint32_t r = o / n_paths;
+    path = o - r * n_paths;
+    return (g * 8u + x) * (uint32_t)VR_XCD_BANDS + r;
+#else
+    const uint32_t c = v * Q + q;
+    const uint32_t sb = c / n_paths;
+    path = c - sb * n_paths;
+    return sb;
+#endif
+}
+
 template <int STACK, uint32_t FEAT, int BT>
 __global__ void __launch_bounds__(BT, path_waves(STACK, cornell_kernel<FEAT>())) render_wave_kernel(const RenderParams p)
 {
@@ -1475,45 +1536,104 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     const uint32_t Q = p.n_queues;                         // power of two, multiple of the 8 XCDs
     const uint32_t n_chunks = n_sub * n_paths;
     (void)n_chunks;
-    uint32_t qj = blockIdx.x & (Q - 1u), drained = 0;
+    uint32_t qj = blockIdx.x & (Q - 1u);
+    // queues this wave knows to be drained (its own failed dequeues and the
+    // launch's drained-queue mask, queue_drained_mask), kept in LDS: the
+    // kernel is at its register limits and this is consulted only at the end
+    __shared__ unsigned long long lds_dead[BT / 64];
+    unsigned long long* const my_dead = lds_dead + (tid >> 6);
+    if (lane == 0) *my_dead = 0ull;
+    uint32_t drained = 0;                                  // whole-frame launches: queues found drained
     auto grab = [&](uint32_t& sub, uint32_t& path) {       // wave-uniform; sub = ~0u when no work is left
         for (;;) {
             uint32_t v = 0;
             if (lane == 0) v = atomicAdd(p.chunk_ctr + qj * kQueueStride, 1u);
-#if VR_XCD_BANDS
-            // queue j serves XCD j % 8 (blocks b % 16 == j under round-robin
-            // dispatch): bands of VR_XCD_BANDS sub-tiles dealt round-robin to
-            // the XCDs, each XCD's chunks sub-major, alternated between its
-            // Q / 8 queues
-            const uint32_t x = qj % 8u, h = qj / 8u;
-            const uint32_t e = __builtin_amdgcn_readfirstlane(v) * (Q / 8u) + h;
-            const uint32_t per_band = (uint32_t)VR_XCD_BANDS * n_paths;
-            const uint32_t g = e / per_band, o = e - g * per_band;
-            const uint32_t r = o / n_paths;
-            const uint32_t sb = (g * 8u + x) * (uint32_t)VR_XCD_BANDS + r;
+            const uint32_t sb = queue_item(qj, __builtin_amdgcn_readfirstlane(v), Q, n_paths, path);
             if (sb < n_sub) {
+#if VR_XCD_BANDS
                 // longest-first: the XCD's sub-tiles in the order of the
                 // previous launch's cost (order_kernel); else band order
-                sub = p.sub_order ? p.sub_order[x * p.order_cap + g * (uint32_t)VR_XCD_BANDS + r] : sb;
-                path = o - r * n_paths;
+                if (p.sub_order) {
+                    const uint32_t x = qj % 8u, r = sb % (uint32_t)VR_XCD_BANDS, g = sb / (8u * (uint32_t)VR_XCD_BANDS);
+                    sub = p.sub_order[x * p.order_cap + g * (uint32_t)VR_XCD_BANDS + r];
+                    return;
+                }
+#endif
+                sub = sb;
                 return;
             }
-#else
-            const uint32_t c = __builtin_amdgcn_readfirstlane(v) * Q + qj;
-            if (c < n_chunks) {
-                sub = c / n_paths;
-                path = c - sub * n_paths;
-                return;
+            // queue qj is drained.  Small launches (one frame per call,
+            // shards: the drain is a large share of them) publish that once
+            // (the first wave to see it) and skip every queue the mask holds: a wave learns that the
+            // launch is out of work from one failed dequeue and one load,
+            // instead of one failed atomic on each of the Q heads -- at the
+            // end of a launch all of its waves did that together, n_waves x Q
+            // atomics on Q words (~88 per us per word), tens of us before the
+            // grid could retire.  Every bit stands for a failed dequeue, so
+            // the wave leaves only when all queues are drained.
+            if constexpr ((FEAT & F_SMALL) == 0u) {
+                // whole-frame launches (a drain of ~1 % of the launch; the
+                // 7-wave kernel has no register to spare): the next queues
+                // in turn, one failed dequeue each
+                if (++drained == Q) { sub = ~0u; path = 0; return; }
+                qj = qj + 1u == Q ? 0u : qj + 1u;
+                continue;
+            }
+#if VR_QSCAN == 1
+            // own-XCD queues only (queue qj + 8k): no cross-XCD stealing
+            if (lane == 0) *my_dead |= 1ull << qj;
+            const uint32_t t0 = __builtin_amdgcn_readfirstlane(lane == 0 ? (uint32_t)*my_dead : 0u);
+            const uint32_t t1 = __builtin_amdgcn_readfirstlane(lane == 0 ? (uint32_t)(*my_dead >> 32) : 0u);
+            const unsigned long long xcd_q = 0x0101010101010101ull << (qj % 8u);
+            const unsigned long long dd = ((unsigned long long)t1 << 32) | t0;
+            if (((all_q_of(Q) & xcd_q) & ~dd) == 0ull) { sub = ~0u; path = 0; return; }
+            {
+                const unsigned long long live = (all_q_of(Q) & xcd_q) & ~dd;
+                const unsigned long long after = qj + 1u < 64u ? (live >> (qj + 1u)) << (qj + 1u) : 0ull;
+                qj = (uint32_t)__builtin_ctzll(after != 0ull ? after : live);
+                continue;
             }
 #endif
-            if (++drained == Q) { sub = ~0u; path = 0; return; }
-            qj = qj + 1u == Q ? 0u : qj + 1u;
+            uint32_t m0 = 0, m1 = 0;
+            if (lane == 0) {
+                unsigned long long* const dmask = queue_drained_mask(p.chunk_ctr);
+                // the first failed dequeue of a queue (exactly one per queue:
+                // no storm of ORs on the mask word when many waves run dry at
+                // once) publishes it; the others read the mask with an
+                // L1-bypassing load (a stale copy only hides drained queues,
+                // which then cost a failed dequeue each, as without the mask)
+                uint32_t pth;
+                const uint32_t v0 = __builtin_amdgcn_readfirstlane(v);
+                const bool first = v0 == 0u || queue_item(qj, v0 - 1u, Q, n_paths, pth) < n_sub;
+                const unsigned long long m = first ? atomicOr(dmask, 1ull << qj)
+                                                   : __hip_atomic_load(dmask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long d = *my_dead | m | (1ull << qj);
+                *my_dead = d;
+                m0 = (uint32_t)d; m1 = (uint32_t)(d >> 32);
+            }
+            const unsigned long long all_q = Q >= 64u ? ~0ull : ((1ull << Q) - 1ull);
+            const unsigned long long live = all_q & ~(((unsigned long long)__builtin_amdgcn_readfirstlane(m1) << 32) |
+                                                      (unsigned long long)__builtin_amdgcn_readfirstlane(m0));
+            if (live == 0ull) { sub = ~0u; path = 0; return; }
+            const unsigned long long after = qj + 1u < 64u ? (live >> (qj + 1u)) << (qj + 1u) : 0ull;
+            qj = (uint32_t)__builtin_ctzll(after != 0ull ? after : live);
         }
     };
 #ifdef VR_WAVE_TIMES
     const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
     const uint64_t wc0 = __builtin_amdgcn_s_memtime();     // shader clock: the wave's effective clock
     uint32_t wpaths = 0, wsteals = 0;
+#endif
+#ifdef VR_WAVE_PHASES
+#if !defined(VR_WAVE_TIMES) || defined(VR_PATH_TIMES)
+#error "VR_WAVE_PHASES needs VR_WAVE_TIMES and excludes VR_PATH_TIMES (same record area)"
+#endif
+    // diagnostic: this wave's shader-clock cycles per phase of the loop (top:
+    // age priority / camera / sphere setup; trav: the mesh loop less help
+    // rounds; help; shade; refill) and its counts (wave-uniform, SGPRs)
+    uint64_t ph_top = 0, ph_trav = 0, ph_help = 0, ph_shade = 0, ph_refill = 0;
+    uint32_t ph_iter = 0, ph_tcalls = 0, ph_shades = 0, ph_setups = 0;
+#define PH_T() __builtin_amdgcn_s_memtime()
 #endif
     uint32_t cur_sub, cur_q;
     grab(cur_sub, cur_q);                                  // wave-uniform: chunk being handed out
@@ -1582,6 +1702,11 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     start(cur_sub, cur_q, (uint32_t)lane);
 
     for (;;) {
+#ifdef VR_WAVE_PHASES
+        uint64_t ph0 = PH_T();
+        ++ph_iter;
+        if (__ballot(state == LS_SETUP || state == LS_CAMERA) != 0ull) ++ph_setups;
+#endif
         if constexpr (track_age<FEAT>()) now_tick = (uint32_t)__builtin_amdgcn_s_memrealtime();
         if constexpr (hold_old<FEAT>()) {
             const bool live = state == LS_SETUP || state == LS_TRAV || state == LS_SHADE || state == LS_CAMERA;
@@ -1611,6 +1736,9 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 state = LS_SHADE;
             }
         }
+#ifdef VR_WAVE_PHASES
+        { const uint64_t t = PH_T(); ph_top += t - ph0; ph0 = t; }
+#endif
         if (HAS(F_MESH)) {
             for (;;) {
                 const int n_trav = __popcll(__ballot(state == LS_TRAV || state == LS_HELP));
@@ -1627,7 +1755,13 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 if constexpr (helpers<FEAT>()) {
                     // (and until helpers a hold started are merged, after it ends)
                     if (cur_sub == ~0u || hold || __ballot(state == LS_HELP || state == LS_HELPDONE) != 0ull) {
+#ifdef VR_WAVE_PHASES
+                        const uint64_t h0 = PH_T();
+#endif
                         const uint32_t given = help_step(p, lane, state, pend, slot, ray, tr, L);
+#ifdef VR_WAVE_PHASES
+                        { const uint64_t t = PH_T(); ph_help += t - h0; ph0 += t - h0; }
+#endif
 #ifdef VR_WAVE_TIMES
                         wsteals += given;
 #else
@@ -1638,6 +1772,9 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #ifdef VR_PATH_COUNTS
                 const uint64_t c1 = __builtin_amdgcn_s_memtime();
                 if (own_trav) cnt.d_ch += (uint32_t)(c1 - c0);
+#endif
+#ifdef VR_WAVE_PHASES
+                ++ph_tcalls;
 #endif
                 if (state == LS_TRAV || state == LS_HELP) {
                     trav_iter<STACK, CNT, FEAT>(p, ray, tr, L, cnt);
@@ -1655,6 +1792,10 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 #endif
             }
         }
+#ifdef VR_WAVE_PHASES
+        { const uint64_t t = PH_T(); ph_trav += t - ph0; ph0 = t; }
+        if (__ballot(state == LS_SHADE) != 0ull) ++ph_shades;
+#endif
         bool ended = false;
 #ifdef VR_PATH_COUNTS
         const uint64_t cs0 = __builtin_amdgcn_s_memtime();
@@ -1711,6 +1852,9 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             if (hold && ended) { state = LS_DONE; ended = false; }
             else if (!hold && cur_sub != ~0u && state == LS_DONE) ended = true;
         }
+#ifdef VR_WAVE_PHASES
+        { const uint64_t t = PH_T(); ph_shade += t - ph0; ph0 = t; }
+#endif
         const unsigned long long em = __ballot(ended);
         if (em != 0ull) {
             const uint32_t need = (uint32_t)__popcll(em);
@@ -1728,8 +1872,36 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             if (next + need > 64u) { cur_sub = nsub; cur_q = nq; next = next + need - 64u; }
             else next += need;
         }
+#ifdef VR_WAVE_PHASES
+        ph_refill += PH_T() - ph0;
+#endif
         if (__ballot(state != LS_DONE) == 0ull) break;
     }
+#ifdef VR_WAVE_PHASES
+    {   // per-wave phase record (8 u64) after the per-wave times
+        uint32_t ms = cnt.w_steps, mp = cnt.w_pairs;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t a = __shfl_xor(ms, off, 64), b = __shfl_xor(mp, off, 64);
+            ms = a > ms ? a : ms; mp = b > mp ? b : mp;
+        }
+        uint32_t nr = cnt.w_nr, lr = cnt.w_lr, nc = cnt.w_nc, lc = cnt.w_lc;
+        for (int off = 32; off > 0; off >>= 1) {
+            nr += __shfl_xor(nr, off, 64); lr += __shfl_xor(lr, off, 64);
+            nc += __shfl_xor(nc, off, 64); lc += __shfl_xor(lc, off, 64);
+        }
+        if (p.counters && lane == 0) {
+            unsigned long long* w = p.counters + kWaveTimesBase + 3 * 8192 + 8 * 8192 + 4 * (blockIdx.x * (uint32_t)(BT / 64) + (uint32_t)(tid >> 6));
+            w[0] = nr; w[1] = lr; w[2] = nc; w[3] = lc;
+        }
+        if (p.counters && lane == 0) {
+            unsigned long long* w = p.counters + kWaveTimesBase + 3 * 8192 + 8 * (blockIdx.x * (uint32_t)(BT / 64) + (uint32_t)(tid >> 6));
+            w[0] = ph_top; w[1] = ph_trav; w[2] = ph_help; w[3] = ph_shade; w[4] = ph_refill;
+            w[5] = (uint64_t)ph_iter | ((uint64_t)ph_tcalls << 32);
+            w[6] = (uint64_t)ms | ((uint64_t)mp << 32);
+            w[7] = (uint64_t)ph_shades | ((uint64_t)ph_setups << 32);
+        }
+    }
+#endif
 #ifdef VR_WAVE_TIMES
     if (p.counters && lane == 0) {   // diagnostic: per-wave start / end (100 MHz) and paths completed
         unsigned long long* w = p.counters + kWaveTimesBase + 3 * (blockIdx.x * (uint32_t)(BT / 64) + (uint32_t)(tid >> 6));

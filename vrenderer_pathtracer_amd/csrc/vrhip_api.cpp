@@ -747,6 +747,8 @@ int vrhip_gl_present(vrhip_ctx* c)
 
 #if defined(VR_WAVE_TIMES) && defined(VR_PATH_TIMES)
 constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192 + (int)(vr::kPathRec * vr::kPathTimesCap);   // + kPathRec per path
+#elif defined(VR_WAVE_TIMES) && defined(VR_WAVE_PHASES)
+constexpr int kDebugSlots = vr::kWaveTimesBase + 15 * 8192;  // + per-wave times, then per-wave phase records (8 + 4 u64)
 #elif defined(VR_WAVE_TIMES)
 constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192;   // + per-wave start / end / paths of render_wave_kernel
 #else
@@ -871,7 +873,7 @@ static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t p
         l.sub_cap = n_sub;
     }
     if (!l.chunk_ctr) {
-        const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * VR_MAX_QUEUES;
+        const size_t bytes = sizeof(uint32_t) * vr::kQueueStride * (VR_MAX_QUEUES + 1);   // heads + drained-queue mask
         HIP_TRY(hipMalloc((void**)&l.chunk_ctr, bytes));
         HIP_TRY(hipMemsetAsync(l.chunk_ctr, 0, bytes, c->stream));
 
@@ -1002,7 +1004,11 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             c->join = false;
         }
         if (p.use_scratch) {
-            if ((rc = ensure_lane(c, l, need, p.path_stride)) != VRHIP_OK) return rc;
+            // every path stream's scratch at once: a lane first used behind a
+            // launch in flight would otherwise allocate there (hipMalloc
+            // waits for the device) and serialise the overlapped launches
+            for (auto& ln : c->lane)
+                if ((rc = ensure_lane(c, ln, need, p.path_stride)) != VRHIP_OK) return rc;
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = reinterpret_cast<vr::vr3*>(l.paths); p.path_w = reinterpret_cast<float*>(p.paths + need);
             p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
@@ -1142,6 +1148,20 @@ extern "C" int vrhip_debug_wave_times(vrhip_ctx* c, uint64_t* out, uint32_t n_wa
     int rc = set_device(c); if (rc) return rc;
     if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
     HIP_TRY(hipMemcpyAsync(out, c->counters + vr::kWaveTimesBase, sizeof(uint64_t) * 3 * n_waves, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return VRHIP_OK;
+}
+#endif
+#if defined(VR_WAVE_TIMES) && defined(VR_WAVE_PHASES)
+// diagnostic build only: per-wave phase records (8 u64 each, then 4 u64 each of
+// node/leaf rounds and cycles; vr_kernel.hip wave_body); out holds 12 x 8192
+extern "C" int vrhip_debug_wave_phases(vrhip_ctx* c, uint64_t* out, uint32_t n_waves)
+{
+    if (!c || !out || n_waves != 8192) return fail(VRHIP_ERR_INVALID, "bad argument");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->counters + vr::kWaveTimesBase + 3 * 8192, sizeof(uint64_t) * 12 * 8192,
+                           hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return VRHIP_OK;
 }
