@@ -28,6 +28,7 @@ WEAK = FARG.startswith("w")
 F0 = int(FARG[1:] if WEAK else FARG)
 SPLIT = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 NS = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
+STEPS = int(os.environ.get("TS_STEPS", "20"))      # timed back-to-back steps per N (bench.py's strong leg: 20)
 sc = scenes.make_scene(cfg)
 W, H = sc["width"], sc["height"]
 px = (W // 16) * 16 * (H // 16) * 16
@@ -40,14 +41,19 @@ for n in NS:
     paths = px * 2 * F
     r.set_tiling(0, n)
     r.clearBuffer()
-    for i in range(2):
-        r.render(frames=F, times=[sc["time"] + i * F + k for k in range(F)])
+    # warm-up: back-to-back steps, so that every path stream has run a launch
+    # of this shape (kernel code loaded, scratch allocated, first-use stream
+    # joins done) before the timed steps
+    W0 = 6
+    for i in range(W0):
+        r.render(frames=F, times=[sc["time"] + i * F + k for k in range(F)], sync=False)
+    r.sync()
     r.kernel_stats(reset=True)
     torch.cuda.synchronize()
-    steps = 6
+    steps = STEPS
     t0 = time.perf_counter()
     for i in range(steps):
-        r.render(frames=F, times=[sc["time"] + (2 + i) * F + k for k in range(F)], sync=False)
+        r.render(frames=F, times=[sc["time"] + (W0 + i) * F + k for k in range(F)], sync=False)
     r.sync()
     dt = (time.perf_counter() - t0) / steps
     kms, launches = r.kernel_stats()

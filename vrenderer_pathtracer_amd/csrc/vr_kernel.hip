@@ -1927,7 +1927,10 @@ __device__ __forceinline__ uint32_t cost_class(uint32_t c)
     const uint32_t msb = 31u - (uint32_t)__builtin_clz(c);
     return 2u * msb + ((c >> (msb - 1u)) & 1u);          // 0..63
 }
-__global__ void __launch_bounds__(1024) order_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
+// 256-thread blocks: a 1,024-thread block needs a whole CU's wave slots, which
+// the next launch's path kernels hold; behind overlapped launches one waited
+// 341 us for them (and every later finish pass behind it on the stream)
+__global__ void __launch_bounds__(256) order_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
                                                       uint32_t n_sub, uint32_t cap)
 {
     __shared__ uint32_t hist[kCostClasses];
@@ -1956,7 +1959,7 @@ __global__ void __launch_bounds__(1024) order_kernel(const uint32_t* __restrict_
 int launch_order(uint32_t* cost, uint32_t* order, uint32_t n_sub, uint32_t cap, void* stream)
 {
     if (n_sub == 0) return 0;
-    hipLaunchKernelGGL(order_kernel, dim3(8), dim3(1024), 0, (hipStream_t)stream, cost, order, n_sub, cap);
+    hipLaunchKernelGGL(order_kernel, dim3(8), dim3(256), 0, (hipStream_t)stream, cost, order, n_sub, cap);
     return (int)hipGetLastError();
 }
 
@@ -2018,6 +2021,12 @@ constexpr uint32_t kFeatHdriMesh = F_MESH;                                      
 constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;        // C3
 constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
 
+// Multi-frame launches of fewer than 2^24 paths (shards) on the small-launch
+// kernels (F_SMALL: helper lanes, per-path costs, longest-first order) or,
+// with 0, on the whole-frame kernels in 256-thread blocks
+#ifndef VR_SHARD_SMALL
+#define VR_SHARD_SMALL 0
+#endif
 template <int STACK, uint32_t FEAT>
 static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 {
@@ -2027,7 +2036,10 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
         if (p.inline_prim) { launch_wave<STACK, FEAT | F_INLINE_PRIM>(p, n_tiles, s); return; }
     }
     if constexpr ((FEAT & (F_SMALL | F_COUNT_EXEC)) == 0u) {
-        if (p.small_blocks) { launch_wave<STACK, FEAT | F_SMALL>(p, n_tiles, s); return; }
+        if (p.small_blocks && (VR_SHARD_SMALL != 0 || (FEAT & F_INLINE_PRIM) != 0u)) {
+            launch_wave<STACK, FEAT | F_SMALL>(p, n_tiles, s);
+            return;
+        }
     }
     if constexpr ((FEAT & F_INLINE_PRIM) == 0u)
         hipLaunchKernelGGL((primary_kernel<STACK, FEAT & ~F_SMALL>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
@@ -2036,7 +2048,9 @@ static void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
     constexpr bool C = cornell_kernel<FEAT>();
     constexpr int BT = ((FEAT & F_SMALL) != 0u) ? wave_block_small(STACK, C) : wave_block(STACK, C);
     constexpr int BTS = wave_block_small(STACK, C);
-    constexpr int B = ((FEAT & F_COUNT_EXEC) != 0u && BTS != BT) ? 0 : BT;   // counted: picked at run time below
+    // counted, or multi-frame shards on the whole-frame kernel: block size picked at run time below
+    constexpr bool runtime_bt = (FEAT & F_COUNT_EXEC) != 0u || ((FEAT & F_SMALL) == 0u && VR_SHARD_SMALL == 0);
+    constexpr int B = (runtime_bt && BTS != BT) ? 0 : BT;
     // blocks per CU: the kernel's full residency, or fewer under a waves-per-SIMD cap
     auto per_cu = [&](int bt) {
         const uint32_t full = (uint32_t)path_blocks_per_cu(STACK, bt, C);

@@ -56,6 +56,10 @@ void dfree(T*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } }
 #endif
 // Path streams (see render_impl): launch i's kernels wait for the finish
 // pass of launch i - VR_PATH_STREAMS, the last reader of the same scratch.
+// multi-frame shards on the small-launch kernels (vr_kernel.hip launch_wave)
+#ifndef VR_SHARD_SMALL
+#define VR_SHARD_SMALL 0
+#endif
 #ifndef VR_PATH_STREAMS
 #define VR_PATH_STREAMS 3
 #endif
@@ -1004,11 +1008,12 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             c->join = false;
         }
         if (p.use_scratch) {
-            // every path stream's scratch at once: a lane first used behind a
-            // launch in flight would otherwise allocate there (hipMalloc
-            // waits for the device) and serialise the overlapped launches
+            // small launches (the ones that overlap): every path stream's
+            // scratch at once -- a lane first used behind a launch in flight
+            // would otherwise allocate there (hipMalloc waits for the device)
+            // and serialise the overlapped launches; whole frames run on lane 0
             for (auto& ln : c->lane)
-                if ((rc = ensure_lane(c, ln, need, p.path_stride)) != VRHIP_OK) return rc;
+                if ((small || &ln == &l) && (rc = ensure_lane(c, ln, need, p.path_stride)) != VRHIP_OK) return rc;
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = reinterpret_cast<vr::vr3*>(l.paths); p.path_w = reinterpret_cast<float*>(p.paths + need);
             p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
@@ -1016,7 +1021,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             // frame per call, shards) measure per sub-tile costs and take their
             // sub-tiles in the order the previous launch on this scratch measured
             const uint32_t n_sub = p.path_stride / 64u;
-            const bool order = wave_kernel && small && count == 0 && c->cost_order;
+            const bool order = wave_kernel && small && count == 0 && c->cost_order && (VR_SHARD_SMALL != 0 || p.inline_prim);
             // per-path costs after the radiances and depth terms in the scratch
             // (need x 16 B holds need x 12 + path_stride x 4 + need x 1)
             p.path_cost = order ? reinterpret_cast<uint8_t*>(p.path_w + p.path_stride) : nullptr;
