@@ -194,11 +194,11 @@ int vrhip_sync(vrhip_ctx *ctx);
 int vrhip_set_path_split(vrhip_ctx *ctx, uint32_t groups);
 /* Overlap of consecutive render launches (no reference counterpart: a
  * scheduling knob; results are unchanged).  The path kernels of launch i+1
- * may start on the second of two internal path streams while launch i drains
+ * may start on another of three internal path streams while launch i drains
  * its last paths; finish passes (accumulation, tonemap) stay in order on the
  * context stream, and any upload, tiling or stream change first waits for
  * the path streams.  mode 1: always, 0: never (launches run one after the
- * other), -1 (default): when a launch has fewer than 2^24 paths (small or
+ * other), -1 (default): when a launch has fewer than 2^25 paths (small or
  * sharded frames, where the drain of a launch is a large share of it). */
 int vrhip_set_overlap(vrhip_ctx *ctx, int mode);
 /* Frames rendered since the last clear (vRendererCuda::getFrameCount,
