@@ -490,6 +490,28 @@ def test_single_tile_and_empty_rank(native, oracle):
     assert nf == 2 and not empty.any()
 
 
+@pytest.mark.parametrize("cfg,w,h,overlap", [("C2", 16, 16, 1), ("C3", 32, 16, -1), ("C2", 48, 32, 0)])
+def test_tiny_one_frame_calls_bitexact(native, oracle, cfg, w, h, overlap):
+    """One-frame launches far smaller than the resident pool: almost every
+    wave finds the queues drained at once and retires through the launch's
+    drained-queue mask (vr_kernel.hip grab), back to back on one or three
+    path streams; the accumulation equals the oracle bit for bit."""
+    sc = scenes.make_scene(cfg, w, h)
+    times = [sc["time"] + 3 * i for i in range(6)]
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.set_overlap(overlap)
+    for t in times:
+        r.render(frames=1, times=[t], sync=False)
+    r.sync()
+    acc = r.read_accum()
+    nf = r.getFrameCount()
+    r.cleanUp()
+    ref, _, _, _ = oracle.render(sc, frames=len(times), times=times, libm=oracle.LIBM_PORTABLE)
+    assert nf == len(times)
+    assert_bitexact(acc, ref, sc, f"{cfg} {w}x{h} one-frame calls")
+
+
 @pytest.mark.parametrize("cfg,w,h", [("C2", 96, 64), ("C3", 96, 64), ("C4", 96, 64)])
 def test_strict_counts_equal_oracle_counts(native, oracle, cfg, w, h):
     """Strict traversal visits exactly the nodes and tests exactly the
