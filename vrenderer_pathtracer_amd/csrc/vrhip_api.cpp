@@ -113,6 +113,8 @@ struct vrhip_ctx {
         uint32_t order_nsub = 0;     // sub-tile count the order was sorted for (0: none)
         hipEvent_t done = nullptr;   // recorded on `s` after the render kernels
         hipEvent_t finished = nullptr;   // recorded on `stream` after the finish pass that read this scratch
+        hipEvent_t ordered = nullptr;    // recorded on `s` after the order pass sorting this scratch's costs
+        bool order_pending = false;      // an order pass was queued since this scratch's last launch
         bool used = false;
     } lane[VR_PATH_STREAMS];
     uint32_t parity = 0;
@@ -479,7 +481,8 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     for (auto& l : c->lane) {
         if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&l.finished, hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&l.finished, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&l.ordered, hipEventDisableTiming) != hipSuccess)
             return cleanup(fail(VRHIP_ERR_HIP, "path stream setup failed"));
     }
     if (hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
@@ -532,6 +535,7 @@ int vrhip_destroy(vrhip_ctx* c)
     for (auto& l : c->lane) {
         dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr); dfree(l.sub_cost); dfree(l.sub_order);
         if (l.done) (void)hipEventDestroy(l.done);
+        if (l.ordered) (void)hipEventDestroy(l.ordered);
         if (l.finished) (void)hipEventDestroy(l.finished);
         if (l.s) (void)hipStreamDestroy(l.s);
     }
@@ -1032,6 +1036,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             p.sub_order = (order && l.order_nsub == n_sub) ? l.sub_order : nullptr;
             p.order_cap = (uint32_t)order_cap(n_sub);
             if (on_lane && l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
+            // the last order pass on this scratch (it read sub_cost, which this
+            // launch's finish pass rewrites, and wrote the order this launch reads)
+            if (l.order_pending) { HIP_TRY(hipStreamWaitEvent(rs, l.ordered, 0)); l.order_pending = false; }
         }
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (n_tiles) {
@@ -1048,14 +1055,22 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         }
         e = vr::launch_finish(p, n_tiles, c->stream);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("finish launch: ") + hipGetErrorString((hipError_t)e));
-        if (p.path_cost) {           // the next launch on this scratch takes this launch's order
-            e = vr::launch_order(p.sub_cost, l.sub_order, p.path_stride / 64u, p.order_cap, c->stream);
-            if (e != 0) return fail(VRHIP_ERR_HIP, std::string("order launch: ") + hipGetErrorString((hipError_t)e));
-            l.order_nsub = p.path_stride / 64u;
-        }
         if (p.use_scratch) {
             HIP_TRY(hipEventRecord(l.finished, c->stream));
             l.used = true;
+        }
+        if (p.path_cost) {
+            // the next launch on this scratch takes this launch's order: sorted
+            // on the path stream behind this finish pass, off the context
+            // stream, so a synchronous caller does not wait for it (one frame
+            // per call: it runs in the host's gap before the next launch,
+            // which waits for it)
+            HIP_TRY(hipStreamWaitEvent(l.s, l.finished, 0));
+            e = vr::launch_order(p.sub_cost, l.sub_order, p.path_stride / 64u, p.order_cap, l.s);
+            if (e != 0) return fail(VRHIP_ERR_HIP, std::string("order launch: ") + hipGetErrorString((hipError_t)e));
+            HIP_TRY(hipEventRecord(l.ordered, l.s));
+            l.order_pending = true;
+            l.order_nsub = p.path_stride / 64u;
         }
         c->frame += k;
         done += k;
