@@ -198,8 +198,9 @@ int vrhip_set_path_split(vrhip_ctx *ctx, uint32_t groups);
  * its last paths; finish passes (accumulation, tonemap) stay in order on the
  * context stream, and any upload, tiling or stream change first waits for
  * the path streams.  mode 1: always, 0: never (launches run one after the
- * other), -1 (default): when a launch has fewer than 2^25 paths (small or
- * sharded frames, where the drain of a launch is a large share of it). */
+ * other), -1 (default): when a launch has fewer than 2^24 paths, or fewer
+ * than 2^25 on a tiled rank (small or sharded frames, where the drain of a
+ * launch is a large share of it). */
 int vrhip_set_overlap(vrhip_ctx *ctx, int mode);
 /* Frames rendered since the last clear (vRendererCuda::getFrameCount,
  * include/vRendererCuda.h:124). */

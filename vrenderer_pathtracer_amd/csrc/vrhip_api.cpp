@@ -987,10 +987,13 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         const bool in_flight = done > 0 || (c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
         // counting launches never overlap: their counters are zeroed on
         // `stream` (above), which a path stream would not wait for
-        // automatic overlap for launches under 2^25 paths (shards; C5's 8-way
-        // shards of 33 M paths: 8-rank projection 0.757 -> 0.78 of linear);
-        // at 66 M paths two persistent launches contend (C5 4-way -17 %)
-        const bool ovl_size = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25);
+        // automatic overlap for launches under 2^24 paths, and under 2^25 for
+        // a rank's shard (C5's 8-way shards of 33 M paths: 8-rank projection
+        // 0.757 -> 0.78 of linear); whole 720p frames of 29.5 M paths lose
+        // with it (C2 -1.7 %, C3 -6 %: two persistent launches contend), as
+        // do C5's 66 M-path 4-way shards (-17 %)
+        const size_t paths_k = (size_t)p.path_stride * 2u * k;
+        const bool ovl_size = paths_k < ((size_t)1 << 24) || (c->nranks > 1 && paths_k < ((size_t)1 << 25));
         const bool ovl = count == 0 && (c->overlap > 0 || (c->overlap < 0 && ovl_size && in_flight));
         p.small_blocks = small ? 1u : 0u;
         p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
