@@ -14,8 +14,11 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libvrhip.so")
-SOURCES = ["vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp", "vr_exr.cpp"]
-HEADERS = ["vr_params.hpp", "vr_math.hpp", "vr_bvh.hpp", "vr_exr.hpp"]
+# the path kernels' scene specialisations are separate translation units
+# (vr_spec_*.hip) so that they compile in parallel
+SOURCES = ["vr_spec_generic.hip", "vr_spec_c2.hip", "vr_spec_c3.hip", "vr_spec_c5.hip", "vr_spec_c1.hip",
+           "vr_spec_c4.hip", "vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp", "vr_exr.cpp"]
+HEADERS = ["vr_params.hpp", "vr_math.hpp", "vr_bvh.hpp", "vr_exr.hpp", "vr_kernel.hpp"]
 ARCH = os.environ.get("VRHIP_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: results are defined without FMA contraction (parity
@@ -47,19 +50,49 @@ def needs_build() -> bool:
     return not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < _newest_input_mtime()
 
 
-def build(force: bool = False, verbose: bool = False, extra_flags=None) -> str:
-    if not force and not needs_build():
+def _jobs() -> int:
+    for var in ("MAX_JOBS", "OMP_NUM_THREADS"):
+        v = os.environ.get(var, "")
+        if v.isdigit() and int(v) > 0:
+            return min(int(v), 16)
+    return max(1, min(os.cpu_count() or 1, 16))
+
+
+def build(force: bool = False, verbose: bool = False, extra_flags=None, out_path: str = None) -> str:
+    """Compile every source to an object in parallel (hipcc -c), then link
+    libvrhip.so.  extra_flags / out_path: variant builds (scripts/build_variants.sh)."""
+    out = out_path or LIB_PATH
+    if not force and out_path is None and not needs_build():
         return LIB_PATH
-    tmp = LIB_PATH + ".tmp"
-    cmd = [_hipcc()] + HIPCC_FLAGS + list(extra_flags or []) + ["-o", tmp] + \
-          [os.path.join(CSRC, s) for s in SOURCES] + ["-lz", "-lrccl"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + res.stdout + res.stderr)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    import concurrent.futures
+    import tempfile
+    hipcc = _hipcc()
+    compile_flags = [f for f in HIPCC_FLAGS if f != "-shared"] + list(extra_flags or [])
+    with tempfile.TemporaryDirectory(prefix="vrhip_build_") as tmpd:
+        objs = [os.path.join(tmpd, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+
+        def compile_one(i):
+            cmd = [hipcc] + compile_flags + ["-c", "-o", objs[i], os.path.join(CSRC, SOURCES[i])]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            return subprocess.run(cmd, capture_output=True, text=True)
+
+        with concurrent.futures.ThreadPoolExecutor(max_workers=_jobs()) as ex:
+            results = list(ex.map(compile_one, range(len(SOURCES))))
+        for src, res in zip(SOURCES, results):
+            if verbose and res.stderr.strip():
+                print(res.stderr, file=sys.stderr)
+            if res.returncode != 0:
+                raise RuntimeError(f"hipcc failed on {src}:\n" + res.stdout + res.stderr)
+        tmp = out + ".tmp"
+        cmd = [hipcc] + HIPCC_FLAGS + list(extra_flags or []) + ["-o", tmp] + objs + ["-lz", "-lrccl"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError("hipcc link failed:\n" + res.stdout + res.stderr)
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -1,0 +1,1728 @@
+// vr_kernel.hpp -- gfx950 (CDNA4, wave64) path-tracing megakernel: device code
+// and kernel templates, shared by vr_kernel.hip (dispatch, finish / order /
+// helper kernels) and the vr_spec_*.hip translation units (one per scene
+// specialisation, compiled in parallel).
+//
+// Re-design of the reference per-pixel CUDA kernel `render`
+// (cuda/src/PathTracer.cu:791-868) and everything it calls:
+//   trace (:597-770), intersectScene (:136-468), SBVH while-while traversal
+//   (:274-463), intersectTriangle (RayIntersection.cuh:54-111), lookupBRDF
+//   (:473-566), hash + thrust minstd RNG (:574-580, :620-622).
+// Results are defined by the reference algorithm in IEEE fp32 (no FMA
+// contraction, correctly rounded div/sqrt, rsqrtf := 1/sqrtf) with the
+// portable libm of vr_math.hpp; the CPU oracle (oracle/vro.c, portable
+// mode) reproduces them bit for bit.
+//
+// MI355X mapping:
+//   * mesh scenes: a persistent path-pool kernel (render_wave_kernel) drains
+//     work queues of 64-path chunks; each lane runs one path at a time
+//     through a resumable state machine and takes the next path when its
+//     own ends (ballot + mbcnt refill), so divergent path lengths do not idle
+//     the SIMD;
+//   * sphere-only scenes: render_kernel, one workgroup per 16x16 pixel tile
+//     (the reference block, so grid truncation is identical), four wave64s
+//     each owning an 8x8 sub-tile;
+//   * the traversal stack lives in LDS, entry-major ([depth][lanes]) so a
+//     wave's push/pop is one conflict-free ds_write/ds_read_b32, next to an
+//     LDS copy of the top of the (area-ordered) tree;
+//   * the while-while traversal switches to leaf processing on a wave64
+//     __ballot (the reference's 32-lane vote.ballot, :353-363);
+//   * leaf hits record only (t, slot, u, v); hit attributes are fetched once
+//     per ray after traversal (result-identical: only the final accepted hit
+//     is observable), cutting gathers on the hot loop;
+//   * all K frames of a render step run in one launch.  Paths store their
+//     radiance to a scratch buffer and finish_kernel adds each pixel's paths
+//     in path order (bit-identical to the reference's in-order sums); one-path-
+//     group sphere launches accumulate in registers instead (render_kernel,
+//     RenderParams::use_scratch = 0).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include "vr_params.hpp"
+#include "vr_math.hpp"
+
+namespace vr {
+
+#define VR_PI 3.14159265359f        // MathHelpers.cuh:16
+#define VR_EPS 0.0000000003f        // MathHelpers.cuh:17
+
+// Scene features are tested twice: against the kernel's compile-time feature
+// set FEAT (code for absent features is compiled out, cutting VGPRs) and
+// against the launch's runtime flags.
+// Feature test inside a kernel specialised on FEAT.  Specialisations marked
+// F_EXACT are launched only when the scene's flags equal their feature set,
+// so their tests fold at compile time; the generic kernel tests the flags.
+constexpr uint32_t F_EXACT = 1u << 31;
+#define HAS(F) ((FEAT & (F)) != 0 && ((FEAT & F_EXACT) != 0 || (p.flags & (F)) != 0))
+
+// ---- float4 with the reference's operator semantics (MathHelpers.cuh:85-196)
+__device__ __forceinline__ vr4 mk4(float x, float y, float z, float w) { vr4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
+__device__ __forceinline__ vr4 add4(vr4 a, vr4 b) { return mk4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ vr4 sub4(vr4 a, vr4 b) { return mk4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
+__device__ __forceinline__ vr4 mul4(vr4 a, vr4 b) { return mk4(a.x * b.x, a.y * b.y, a.z * b.z, a.w); }
+__device__ __forceinline__ vr4 mul4s(vr4 a, float b) { return mk4(a.x * b, a.y * b, a.z * b, a.w); }
+__device__ __forceinline__ vr4 muls4(float a, vr4 b) { return mk4(a * b.x, a * b.y, a * b.z, b.w); }
+__device__ __forceinline__ void muleq4(vr4& a, vr4 b) { a.x *= b.x; a.y *= b.y; a.z *= b.z; a.w *= b.w; }
+__device__ __forceinline__ void muleq4s(vr4& a, float b) { a.x *= b; a.y *= b; a.z *= b; }
+__device__ __forceinline__ float dot4(vr4 a, vr4 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ vr4 cross4(vr4 a, vr4 b) {
+    return mk4(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x, 0.0f);
+}
+__device__ __forceinline__ vr4 normalize4(vr4 a) { const float inv = inv_sqrt_exact(dot4(a, a)); return mul4s(a, inv); }
+__device__ __forceinline__ float clampi(int v, int lo, int hi) { const int m = hi < v ? hi : v; return (float)(lo > m ? lo : m); }
+__device__ __forceinline__ float clampf(float v, float lo, float hi) { return __builtin_fmaxf(lo, __builtin_fminf(hi, v)); }
+__device__ __forceinline__ vr4 tbn_mul(vr4 m0, vr4 m1, vr4 m2, vr4 b) {   // mat4 * float4, m3 = (0,0,0,1)
+    return mk4(m0.x * b.x + m1.x * b.y + m2.x * b.z + 0.0f * b.w,
+               m0.y * b.x + m1.y * b.y + m2.y * b.z + 0.0f * b.w,
+               m0.z * b.x + m1.z * b.y + m2.z * b.z + 0.0f * b.w,
+               m0.w * b.x + m1.w * b.y + m2.w * b.z + 1.0f * b.w);
+}
+
+// Kepler span helpers on integer bit patterns (MathHelpers.cuh:454-552):
+// v_min/v_max_f32 per axis, then v_max3/v_min3_i32 on the bits.
+__device__ __forceinline__ float span_begin(float a0, float a1, float b0, float b1, float c0, float c1, float d) {
+    const int zc = max(min(__float_as_int(c0), __float_as_int(c1)), __float_as_int(d));
+    return __int_as_float(max(max(__float_as_int(__builtin_fminf(a0, a1)), __float_as_int(__builtin_fminf(b0, b1))), zc));
+}
+__device__ __forceinline__ float span_end(float a0, float a1, float b0, float b1, float c0, float c1, float d) {
+    const int zc = min(max(__float_as_int(c0), __float_as_int(c1)), __float_as_int(d));
+    return __int_as_float(min(min(__float_as_int(__builtin_fmaxf(a0, a1)), __float_as_int(__builtin_fmaxf(b0, b1))), zc));
+}
+
+// ---- scene constants (PathTracer.cu:107-123)
+struct Sph { float r, px, py, pz, ex, ey, ez, cr, cg, cb; int refl; };
+__device__ __forceinline__ Sph cornell_sphere(int i) {
+    switch (i) {
+    case 0: return { 160.f, 0.f, 160.f + 49.f, 0.f, 4.f, 3.6f, 3.2f, 0.f, 0.f, 0.f, 1 };
+    case 1: return { 1e5f, 1e5f + 50.f, 0.f, 0.f, 0.075f, 0.025f, 0.025f, 0.75f, 0.25f, 0.25f, 1 };
+    case 2: return { 1e5f, -1e5f - 50.f, 0.f, 0.f, 0.025f, 0.075f, 0.025f, 0.25f, 0.75f, 0.25f, 1 };
+    case 3: return { 1e5f, 0.f, 0.f, -1e5f - 100.f, 0.f, 0.f, 0.f, 1.f, 1.f, 1.f, 1 };
+    case 4: return { 1e5f, 0.f, 1e5f + 50.f, 0.f, 0.f, 0.f, 0.f, 1.f, 1.f, 1.f, 1 };
+    default: return { 1e5f, 0.f, -1e5f - 50.f, 0.f, 0.f, 0.f, 0.f, 1.f, 1.f, 1.f, 1 };
+    }
+}
+__device__ __forceinline__ Sph small_sphere(int i) {
+    if (i == 0) return { 3.5f, 15.f, 0.f, 15.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0 };   // mirror
+    return { 3.5f, 25.f, 0.f, 15.f, 0.f, 0.f, 0.f, 1.f, 1.f, 1.f, 1 };             // grey, Fresnel
+}
+__device__ __forceinline__ Sph example_sphere() { return { 10.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1.f, 1.f, 1.f, 1 }; }
+
+struct Ray { vr4 o, d; };
+
+// Sphere::intersect (PathTracer.cu:87-104)
+__device__ __forceinline__ float sphere_intersect(const Sph& s, const Ray& r) {
+    const vr4 op = sub4(mk4(s.px, s.py, s.pz, 0.f), r.o);
+    const float eps = (float)1e-4;
+    const float b = dot4(op, r.d);
+    float det = b * b - dot4(op, op) + s.r * s.r;
+    if (det < 0) return 0;
+    det = sqrt_exact(det);
+    float t;
+    return (t = b - det) > eps ? t : ((t = b + det) > eps ? t : 0.0f);
+}
+
+enum HitKind { HK_NONE = 0, HK_CORNELL = 1, HK_SMALL = 2, HK_EXAMPLE = 3, HK_MESH = 4 };
+struct HitRec {
+    float t;
+    int kind, idx;          // sphere index or triangle slot
+    float bu, bv;           // barycentrics for mesh hits
+    float su, sv;           // example sphere texture coords (from the stale normal)
+};
+// Per-lane event counts for the counting variant (algorithmic bytes).
+struct Cnt {
+    uint32_t rays = 0, nodes = 0, slots = 0, tris = 0, attr = 0, tex = 0, hdr = 0, brdf = 0;
+    // instrumented production kernels (F_COUNT_EXEC) only
+    // and its lane loads by width (16 / 12 / 8 / 4 B) at every global-load site
+    uint32_t nodes_lds = 0, tri_loads = 0, mesh_hits = 0, nmap_hits = 0, ld128 = 0, ld96 = 0, ld64 = 0, ld32 = 0;
+    // the path kernel's cost of the lane's current path (node visits), summed
+    // per sub-tile for the next launch's longest-first order (RenderParams::sub_cost)
+    uint32_t work = 0;
+};
+
+// Counting launches (COUNT) come in two kinds: the reference algorithm's
+// event counts (no primary-hit reuse, no last-bounce shortcut)
+// and the instrumented production kernels (F_COUNT_EXEC in FEAT), which run
+// exactly what vrhip_render runs and count the memory operations issued.
+template <bool COUNT, uint32_t FEAT>
+__device__ constexpr bool ref_alg() { return COUNT && (FEAT & F_COUNT_EXEC) == 0u; }
+
+// One wave-level reduction and one 64-bit atomic per counter per wave.
+__device__ __forceinline__ void flush_counts(const RenderParams& p, const Cnt& cnt, int lane, bool exec)
+{
+    const uint32_t v[kCounters + kExecCounters] = { cnt.rays, cnt.nodes, cnt.slots, cnt.tris, cnt.attr, cnt.tex,
+                                                    cnt.hdr, cnt.brdf, cnt.nodes_lds, cnt.tri_loads,
+                                                    cnt.mesh_hits, cnt.nmap_hits, cnt.ld128, cnt.ld96, cnt.ld64,
+                                                    cnt.ld32 };
+#pragma unroll
+    for (int k = 0; k < kCounters + kExecCounters; ++k) {
+        if (k >= kCounters && !exec) break;
+        unsigned long long x = v[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+        const int slot = k < kCounters ? k : kExecCounterBase + (k - kCounters);
+        if (lane == 0 && x) atomicAdd(p.counters + slot, x);
+    }
+}
+
+struct Hit {                // vHitData, PathTracer.cuh:17-53
+    vr4 hp, n, tan, em, col, spec;
+    unsigned type;
+};
+
+__device__ __forceinline__ int tex_addr(uint32_t w, uint32_t h, float u, float v) {
+    const int x = f2i((float)w * u);
+    const int y = f2i((float)h * v);
+    const int val = (int)((uint32_t)x + (uint32_t)y * w);
+    return (int)clampi(val, 0, (int)(w * h - 1u));
+}
+
+// Normal of a sphere hit (the value the reference leaves in m_normal).
+__device__ __forceinline__ vr4 sphere_normal(const HitRec& hr, const Ray& r) {
+    const Sph s = hr.kind == HK_CORNELL ? cornell_sphere(hr.idx) : small_sphere(hr.idx);
+    const vr4 hp = add4(r.o, mul4s(r.d, hr.t));
+    return normalize4(sub4(hp, mk4(s.px, s.py, s.pz, 0.f)));
+}
+
+// Device mesh layout (built from the reference layout at upload, vrhip_api.cpp):
+//   nodes: the reference's 4 x float4 per inner node, except that a leaf
+//          child is ~((first_tri << 7) | tri_count) into the compact arrays;
+//   tris:  3 float4 vertex positions per triangle, leaves contiguous, in the
+//          reference's slot order (no terminator slots);
+//   attributes (normals, tangents, uvs): same indexing, fetched only for the
+//          final hit of a ray.
+// The triangles tested and their order are those of the reference layout, so
+// the closest hit (ties included) is unchanged.
+constexpr int kLeafCountBits = 7;
+
+// Per-block LDS: the traversal stacks (entry-major, one column per thread)
+// and a copy of the first nodes of the area-ordered node array (rows 0-2 and
+// the two child indices, 56 B per node).  The node cache takes what is left
+// of a 40 KB budget, so four blocks (16 waves) still fit a CU's 160 KB.
+#ifndef VR_LDS_BUDGET
+#define VR_LDS_BUDGET (40960 - 256)
+#endif
+constexpr int kLdsBudget = VR_LDS_BUDGET;
+constexpr int cache_nodes(int stack, int extra = 0, int bt = kBlockThreads) {
+    return ((bt / kBlockThreads) * kLdsBudget - stack * bt * 4 - extra) / 56 > 0 ?
+           ((bt / kBlockThreads) * kLdsBudget - stack * bt * 4 - extra) / 56 : 1;
+}
+// Raw buffer loads for the node and triangle arrays: a 32-bit lane offset
+// against an SGPR descriptor (bounds-checked, no 64-bit address math), and an
+// explicit width per fetch (16 B node rows and triangle-pair rows, 8 B child
+// indices and pair tails).
+typedef unsigned int vr_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int vr_u32x3 __attribute__((ext_vector_type(3)));
+typedef unsigned int vr_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ vr4 buf_load4(__amdgpu_buffer_rsrc_t b, int off) {
+    const vr_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, 0);
+    return mk4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ int2 buf_load2i(__amdgpu_buffer_rsrc_t b, int off) {
+    const vr_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(b, off, 0, 0);
+    return make_int2((int)v.x, (int)v.y);
+}
+
+// The t-culled traversal (default) reads conservative fp16 node boxes: two
+// 16-B loads per node visit instead of four, the vector-memory instructions
+// this kernel is bound by (C2 +9 %, C3 +5 %, C5 +5 % on the 6-wave kernel).
+// Rounded outward, a box only grows, so no hit is lost; the looser boxes
+// change the visit order, which the exact equal-t tie-break (ref_first) makes
+// irrelevant to the result: images equal the fp32 and the strict traversal
+// bit for bit (C5 differed in one pixel in 8.3 M without it).  The strict
+// traversal (F_STRICT) reads the reference's fp32 rows.
+
+struct Lds {
+    int* stk;                 // this thread's column of the stack
+    const vr4* nodes;         // fp32 nodes: 3 rows per cached node; fp16 nodes: 2 rows per node
+    const int2* idx;          // fp32 nodes: child indices per cached node
+    int n_cached;             // nodes [0, n_cached) are read from LDS
+    int stride;               // stack entry stride (threads per block; entry-major [depth][threads])
+};
+
+// CudaTracerLib-style while-while traversal (PathTracer.cu:276-463), split
+// into init / one outer iteration / finish so a wave can pause it between
+// outer iterations (render_wave_kernel) without changing any lane's sequence
+// of node visits and triangle tests.
+constexpr int kSentinel = 0x76543210;
+struct Trav {
+    float ivx, ivy, ivz, odx, ody, odz;
+    float t, tcull, bu, bv;
+    int best, sp, nodeAddr;
+};
+
+template <uint32_t FEAT>
+__device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, float t0, Trav& tr, const Lds& L)
+{
+    tr.sp = 0;
+    L.stk[0] = kSentinel;
+    tr.nodeAddr = 0;
+    // invDir (PathTracer.cu:289-294): components with |d| <= eps become +eps,
+    // so |d| >= eps > 2^-32 and rcp_rn is the IEEE quotient unless a
+    // component exceeds 2^125 (then the wave divides)
+    const float dx = __builtin_fabsf(r.d.x) > VR_EPS ? r.d.x : VR_EPS;
+    const float dy = __builtin_fabsf(r.d.y) > VR_EPS ? r.d.y : VR_EPS;
+    const float dz = __builtin_fabsf(r.d.z) > VR_EPS ? r.d.z : VR_EPS;
+    if (__builtin_expect(__ballot(!(__builtin_fabsf(dx) <= kRcpRnHi && __builtin_fabsf(dy) <= kRcpRnHi &&
+                                    __builtin_fabsf(dz) <= kRcpRnHi)) != 0ull, 0)) {
+        tr.ivx = 1.f / dx; tr.ivy = 1.f / dy; tr.ivz = 1.f / dz;
+    } else {
+        tr.ivx = rcp_rn(dx); tr.ivy = rcp_rn(dy); tr.ivz = rcp_rn(dz);
+    }
+    tr.odx = r.o.x * tr.ivx; tr.ody = r.o.y * tr.ivy; tr.odz = r.o.z * tr.ivz;
+    tr.t = t0;
+    // t-culling: a child whose slab entry lies beyond the closest hit so far
+    // (times a 2^-10 safety margin) cannot hold a closer triangle.  The
+    // reference visits every pierced box (span end clamped to 1e20,
+    // :316,322); F_STRICT restores that exactly.
+    tr.tcull = HAS(F_STRICT) ? __builtin_inff() : t0 * 1.0009765625f;
+    tr.best = -1;
+    tr.bu = tr.bv = 0.f;
+}
+
+// Pop (:339-342 and the leaf-loop pops).  sp reaches -1 only by popping the
+// sentinel, after which nothing is popped.
+__device__ __forceinline__ int trav_pop(Trav& tr, const Lds& L)
+{
+    return L.stk[(tr.sp--) * L.stride];
+}
+
+// One inner-node visit (:295-343): fetch (LDS copy or L2/HBM), two slab
+// tests, near child next, far child pushed when both are entered, pop when
+// neither is.  Leaves in tr.nodeAddr are left to the caller.
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
+{
+    int* stk = L.stk;
+    const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
+    if (COUNT) cnt.nodes += 1u;
+    if ((FEAT & F_SMALL) != 0u) cnt.work++;
+    vr4 n0, n1, nz;
+    int idx0, idx1;
+    const int node = tr.nodeAddr >> 2;
+    // wave-uniform choice between the LDS copy and L2/HBM: a diverged wave
+    // would pay both round trips
+    const bool in_lds = __ballot(node >= L.n_cached) == 0ull;
+    if (COUNT) {
+        cnt.nodes_lds += in_lds ? 1u : 0u;
+        if (!in_lds) { cnt.ld128 += strict ? 3u : 2u; cnt.ld64 += strict ? 1u : 0u; }
+    }
+    if (!strict) {
+        // conservative fp16 boxes (lows rounded down, highs up): two 16-B
+        // fetches per node instead of four; a box can only grow, so no hit
+        // the exact box admits is lost
+        vr4 a, b;
+        if (in_lds) {
+            a = L.nodes[2 * node];
+            b = L.nodes[2 * node + 1];
+        } else {
+            const __amdgpu_buffer_rsrc_t hbuf = buf_rsrc(p.bvh16, p.n_nodes * 32u);
+            const int off = node * 32;
+            a = buf_load4(hbuf, off);
+            b = buf_load4(hbuf, off + 16);
+        }
+        auto lo = [](float w) { return __half2float(__ushort_as_half((unsigned short)(__float_as_uint(w) & 0xffffu))); };
+        auto hi = [](float w) { return __half2float(__ushort_as_half((unsigned short)(__float_as_uint(w) >> 16))); };
+        n0 = mk4(lo(a.x), hi(a.x), lo(a.y), hi(a.y));          // c0 x, y
+        nz = mk4(lo(a.z), hi(a.z), lo(b.y), hi(b.y));          // c0 z, c1 z
+        n1 = mk4(lo(a.w), hi(a.w), lo(b.x), hi(b.x));          // c1 x, y
+        idx0 = __float_as_int(b.z);
+        idx1 = __float_as_int(b.w);
+    } else {
+        int2 ni;
+        if (in_lds) {
+            const int row = __mul24(3, node);                 // v_mul_u32_u24 (full rate)
+            n0 = L.nodes[row + 0];
+            n1 = L.nodes[row + 1];
+            nz = L.nodes[row + 2];
+            ni = L.idx[node];
+        } else {
+            const __amdgpu_buffer_rsrc_t nbuf = buf_rsrc(p.bvh, p.n_nodes * 64u);
+            const int off = tr.nodeAddr * 16;                 // byte offset of the node
+            n0 = buf_load4(nbuf, off);
+            n1 = buf_load4(nbuf, off + 16);
+            nz = buf_load4(nbuf, off + 32);
+            ni = buf_load2i(nbuf, off + 48);                  // 8 of the row's 16 bytes are used
+        }
+        idx0 = ni.x;
+        idx1 = ni.y;
+    }
+    // slab distances n*inv - o*inv (:307-322); the culled mode lets
+    // them contract to one v_fma each (more accurate)
+    auto slab = [&](float n, float iv, float od) {
+        return strict ? (n * iv - od) : __builtin_fmaf(n, iv, -od);
+    };
+    const float c0lox = slab(n0.x, tr.ivx, tr.odx);
+    const float c0hix = slab(n0.y, tr.ivx, tr.odx);
+    const float c0loy = slab(n0.z, tr.ivy, tr.ody);
+    const float c0hiy = slab(n0.w, tr.ivy, tr.ody);
+    const float c0loz = slab(nz.x, tr.ivz, tr.odz);
+    const float c0hiz = slab(nz.y, tr.ivz, tr.odz);
+    const float c1loz = slab(nz.z, tr.ivz, tr.odz);
+    const float c1hiz = slab(nz.w, tr.ivz, tr.odz);
+    const float c0min = span_begin(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, 0.0f);
+    const float c0max = span_end(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, 1e20f);
+    const float c1lox = slab(n1.x, tr.ivx, tr.odx);
+    const float c1hix = slab(n1.y, tr.ivx, tr.odx);
+    const float c1loy = slab(n1.z, tr.ivy, tr.ody);
+    const float c1hiy = slab(n1.w, tr.ivy, tr.ody);
+    const float c1min = span_begin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 0.0f);
+    const float c1max = span_end(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, 1e20f);
+    // keep the child-index load in the same round trip as the bounds
+    asm volatile("" ::"v"(idx0), "v"(idx1));
+    const bool swp = (c1min < c0min);
+    const bool tc0 = (c0max >= c0min) && (c0min <= tr.tcull);
+    const bool tc1 = (c1max >= c1min) && (c1min <= tr.tcull);
+    // branch-free push/pop: near child next, far child pushed when both
+    // are hit, pop when neither is (same order as :324-343)
+    const bool both = tc0 && tc1;
+    const bool none = !tc0 && !tc1;
+    const int nearc = (both && swp) ? idx1 : (tc0 ? idx0 : idx1);
+    const int farc = swp ? idx0 : idx1;
+    const int top = stk[tr.sp * L.stride];
+    if (both) stk[(tr.sp + 1) * L.stride] = farc;
+    tr.sp += both ? 1 : (none ? -1 : 0);
+    tr.nodeAddr = none ? top : nearc;
+}
+
+// Equal-t tie-break of the culled traversal.  The reference keeps the first
+// of two triangles hit at exactly the same distance (strict `<`,
+// PathTracer.cu:379), i.e. the one its depth-first walk tests first: slot
+// order inside a leaf; otherwise the child of the two leaves' lowest common
+// ancestor that the walk enters first for this ray -- the nearer by slab entry,
+// child 0 on equal entries (:324-343), computed here with the reference's own
+// (uncontracted) slab arithmetic.  The t-culled walk skips boxes and its
+// contracted slabs can order near-equal children differently, so it asks
+// this whenever a triangle ties the closest hit: any visit order then yields
+// the reference's hit.  Rare (exact fp32 ties: rays through shared edges).
+__device__ __forceinline__ bool ref_first(const RenderParams& p, const Trav& tr, int ka, int kb)
+{
+    const unsigned long long a = p.tpath[ka], b = p.tpath[kb];
+    if (a == b) return ka < kb;                                    // one leaf: slot order
+    const int L = __builtin_ctzll(a ^ b);                          // depth where the paths part
+    const int da = 63 - __builtin_clzll(a), db = 63 - __builtin_clzll(b);
+    if (L >= da || L >= db) return ka < kb;                        // not a tree path (cannot happen)
+    const __amdgpu_buffer_rsrc_t nbuf = buf_rsrc(p.bvh, p.n_nodes * 64u);
+    int off = 0;                                                   // byte offset of the root
+    for (int i = 0; i < L; ++i) {
+        const int2 ni = buf_load2i(nbuf, off + 48);
+        off = (((a >> i) & 1ull) ? ni.y : ni.x) * 16;              // child float4 offset -> bytes
+    }
+    const vr4 n0 = buf_load4(nbuf, off), n1 = buf_load4(nbuf, off + 16), nz = buf_load4(nbuf, off + 32);
+    auto sl = [](float n, float iv, float od) { return n * iv - od; };   // -ffp-contract=off: no FMA
+    const float c0min = span_begin(sl(n0.x, tr.ivx, tr.odx), sl(n0.y, tr.ivx, tr.odx), sl(n0.z, tr.ivy, tr.ody),
+                                   sl(n0.w, tr.ivy, tr.ody), sl(nz.x, tr.ivz, tr.odz), sl(nz.y, tr.ivz, tr.odz), 0.0f);
+    const float c1min = span_begin(sl(n1.x, tr.ivx, tr.odx), sl(n1.y, tr.ivx, tr.odx), sl(n1.z, tr.ivy, tr.ody),
+                                   sl(n1.w, tr.ivy, tr.ody), sl(nz.z, tr.ivz, tr.odz), sl(nz.w, tr.ivz, tr.odz), 0.0f);
+    const unsigned first = (c1min < c0min) ? 1u : 0u;
+    return (unsigned)((a >> L) & 1ull) == first;
+}
+
+// intersectTriangle (RayIntersection.cuh:54-111) for compact triangle k and
+// the closest-hit update (:379-386).  Evaluated branch-free: every early
+// return of the reference becomes a term of the final predicate (the values
+// computed for a surviving triangle are the same operations in the same order).
+struct TriV { vr3 a0, a1, a2; };        // v0, e1 = v1 - v0, e2 = v2 - v0 (p.tri_e)
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, Trav& tr, int k, const TriV& t, Cnt& cnt)
+{
+    const bool strict = HAS(F_STRICT);
+    if (COUNT) cnt.tris++;
+    const vr4 v0 = mk4(t.a0.x, t.a0.y, t.a0.z, 0.f);
+    const vr4 e1 = mk4(t.a1.x, t.a1.y, t.a1.z, 0.f);         // v1 - v0, v2 - v0 (RayIntersection.cuh:62-63), from the upload
+    const vr4 e2 = mk4(t.a2.x, t.a2.y, t.a2.z, 0.f);
+    const vr4 pv = cross4(r.d, e2);
+    const float det = dot4(e1, pv);
+    // 1/det (RayIntersection.cuh:75): only lanes with |det| >= VR_EPS (> 2^-32) can accept the
+    // hit, and there rcp_rn is the IEEE quotient up to |det| = 2^125; a wave
+    // holding a larger (or non-finite) det takes the division
+    float inv_det;
+    if (__builtin_expect(__ballot(!(__builtin_fabsf(det) <= kRcpRnHi)) != 0ull, 0)) inv_det = 1.f / det;
+    else inv_det = rcp_rn(det);
+    const vr4 tv = sub4(r.o, v0);
+    const float u = dot4(tv, pv) * inv_det;
+    const vr4 q = cross4(tv, e1);
+    const float v = dot4(r.d, q) * inv_det;
+    const float dist = dot4(e2, q) * inv_det;
+    const bool ok = !(det > -VR_EPS && det < VR_EPS) && !(u < 0.f || u > 1.f) &&
+                    !(v < 0.f || u + v > 1.f);
+    if (ok && dist > VR_EPS && dist < tr.t) {
+        tr.t = dist; tr.best = 3 * k; tr.bu = u; tr.bv = v;
+        tr.tcull = strict ? tr.tcull : tr.t * 1.0009765625f;
+    }
+    // a tie with the mesh's closest hit so far: keep the reference's first
+    // (the strict walk tests in the reference order already)
+    const bool tie = !strict && ok && dist > VR_EPS && dist == tr.t && tr.best >= 0 && 3 * k != tr.best;
+    if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
+        if (tie && ref_first(p, tr, k, tr.best / 3)) { tr.best = 3 * k; tr.bu = u; tr.bv = v; }
+    }
+}
+
+// One outer iteration of the while-while loop: the inner node loop until
+// this lane holds a leaf and the wave agrees (ballot, :353-363), with one
+// leaf postponed (:345-351), then the leaf loop.  tr.nodeAddr is an inner
+// node, a leaf (a helper's first entry) or kSentinel (no-op).
+#ifndef VR_NODE_BREAK
+#define VR_NODE_BREAK 6    // measured (path kernel with paired triangle loads): 0 (the reference's
+                           // all-lanes vote) C2 2,294, 2: 2,503, 4: 2,563, 6: 2,577, 8: 2,583 (C3 -2 %)
+#endif
+#ifndef VR_NODE_BREAK_CORNELL
+// Cornell-box kernels (every bounce ray stays inside the box and most lanes
+// keep traversing the mesh): r02 6-wave kernel, C2 6: 3,910, 10: 3,986;
+// the HDRI scenes lose at 10 (C3 -1.3 %, C5 -1.2 %) and keep VR_NODE_BREAK
+#define VR_NODE_BREAK_CORNELL 10
+#endif
+template <uint32_t FEAT>
+constexpr int node_break() {
+    // one-frame kernels (F_INLINE_PRIM) keep 6: the interactive C2 rate fell
+    // 2,147 -> 2,103 Mpaths/s with 10 (r02h)
+    return ((FEAT & F_EXACT) && (FEAT & F_CORNELL) && !(FEAT & F_INLINE_PRIM)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK;
+}
+// The node-loop exit is proportional to the lanes in the call: a full wave
+// leaves once at most node_break of its 64 lanes still search (throughput:
+// the rest of the wave need not wait for its slowest searches), a wave with
+// few traversing lanes -- the sparse waves of a launch's drain, or a wave
+// whose other lanes are shading -- waits for all of them, as the reference's
+// vote does (:353-363).  A fixed threshold made a sparse wave's lanes leave
+// after ONE node visit per outer iteration: the most expensive paths (C2:
+// ~200 node visits, ~100 triangle tests) then needed 50-150 outer iterations
+// and ran 300-770 us, the critical path of a one-frame launch (r03 drain
+// diagnostics, removed in r04; git history).
+#ifndef VR_NODE_BREAK_PROP
+#define VR_NODE_BREAK_PROP 1
+#endif
+template <int STACK, bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void trav_iter(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
+{
+#if VR_NODE_BREAK_PROP
+    const int brk = node_break<FEAT>() * __popcll(__ballot(1));  // exit when searching * 64 <= brk
+#else
+    const int brk = node_break<FEAT>() * 64;
+#endif
+    int leafAddr = 0;
+    if (tr.nodeAddr < 0) {                                      // a leaf to start with (a helper's subtree)
+        leafAddr = tr.nodeAddr;
+        tr.nodeAddr = trav_pop(tr, L);
+    }
+    while ((unsigned)tr.nodeAddr < (unsigned)kSentinel) {
+        node_step<COUNT, FEAT>(p, r, tr, L, cnt);
+        if (tr.nodeAddr < 0 && leafAddr >= 0) {                 // postpone max 1
+            leafAddr = tr.nodeAddr;
+            tr.nodeAddr = trav_pop(tr, L);
+        }
+        // the wave moves on to the leaves once (nearly) every lane holds one;
+        // lanes still searching resume in the next outer iteration
+        if (__popcll(__ballot(leafAddr >= 0)) * 64 <= brk) break;
+    }
+    while (leafAddr < 0) {
+        const int lv = ~leafAddr;
+        const int kend = (lv >> kLeafCountBits) + (lv & ((1 << kLeafCountBits) - 1));
+        // the loads of two triangles in one trip (the tests stay in slot order):
+        // a leaf's triangles need half the dependent round trips (C2 +1 %, C3 +4 %),
+        // the pair's 72 contiguous bytes as 4 x 16 B + 8 B (5 loads instead of 6:
+        // C2 +1 %, C3 +1 %, C5 +3 %); past the array end the buffer descriptor
+        // returns zeros (never tested)
+        for (int k = lv >> kLeafCountBits; k < kend; k += 2) {
+            const bool two = k + 1 < kend;
+            TriV ta, tb;
+            {
+                const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, p.n_tris * 36u);
+                const int o = k * 36;
+                const vr4 q0 = buf_load4(tbuf, o), q1 = buf_load4(tbuf, o + 16), q2 = buf_load4(tbuf, o + 32),
+                          q3 = buf_load4(tbuf, o + 48);
+                const int2 q4 = buf_load2i(tbuf, o + 64);
+                ta.a0 = vr3{ q0.x, q0.y, q0.z }; ta.a1 = vr3{ q0.w, q1.x, q1.y }; ta.a2 = vr3{ q1.z, q1.w, q2.x };
+                tb.a0 = vr3{ q2.y, q2.z, q2.w }; tb.a1 = vr3{ q3.x, q3.y, q3.z };
+                tb.a2 = vr3{ q3.w, __int_as_float(q4.x), __int_as_float(q4.y) };
+            }
+            if (COUNT) {                                        // an odd leaf's last pair loads its triangle twice
+                cnt.tri_loads += 2;
+                cnt.ld128 += 4; cnt.ld64 += 1;
+            }
+            asm volatile("" ::"v"(ta.a0.x), "v"(ta.a1.x), "v"(ta.a2.x), "v"(tb.a0.x), "v"(tb.a1.x), "v"(tb.a2.x));
+            tri_test_v<COUNT, FEAT>(p, r, tr, k, ta, cnt);
+            if (two) tri_test_v<COUNT, FEAT>(p, r, tr, k + 1, tb, cnt);
+        }
+        leafAddr = tr.nodeAddr;
+        if (tr.nodeAddr < 0) tr.nodeAddr = trav_pop(tr, L);
+    }
+}
+
+__device__ __forceinline__ void trav_finish(const Trav& tr, HitRec& hr)
+{
+    if (tr.best >= 0) { hr.t = tr.t; hr.kind = HK_MESH; hr.idx = tr.best; hr.bu = tr.bu; hr.bv = tr.bv; }
+}
+
+template <int STACK, bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
+{
+    Trav tr;
+    trav_init<FEAT>(p, r, hr.t, tr, L);
+    while (tr.nodeAddr != kSentinel) trav_iter<STACK, COUNT, FEAT>(p, r, tr, L, cnt);
+    trav_finish(tr, hr);
+}
+// intersectScene (PathTracer.cu:136-468): closest hit, attributes deferred.
+// intersectScene (PathTracer.cu:136-468), sphere part: Cornell walls and
+// light, the two small spheres, the example sphere.  Returns true when the
+// mesh must still be traversed (kMeshInitialised and no example sphere).
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool intersect_spheres(const RenderParams& p, const Ray& r, HitRec& hr, Cnt& cnt)
+{
+    if (COUNT) cnt.rays++;
+    hr.t = 1e20f; hr.kind = HK_NONE; hr.idx = 0; hr.bu = hr.bv = 0.f; hr.su = hr.sv = 0.f;
+    if HAS(F_CORNELL) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const float dist = sphere_intersect(cornell_sphere(i), r);
+            if (dist != 0.f && dist < hr.t) { hr.t = dist; hr.kind = HK_CORNELL; hr.idx = i; }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const float dist = sphere_intersect(small_sphere(i), r);
+        if (dist != 0.f && dist < hr.t) { hr.t = dist; hr.kind = HK_SMALL; hr.idx = i; }
+    }
+    if HAS(F_EXAMPLE) {
+        const float dist = sphere_intersect(example_sphere(), r);
+        if (dist != 0.f && dist < hr.t) {
+            if (HAS(F_TEX_DIFF) || HAS(F_TEX_NORM) || HAS(F_TEX_SPEC)) {
+                // u,v from the normal left by the previous hit of this call (:202-204)
+                const vr4 sn = hr.kind == HK_NONE ? mk4(0.f, 0.f, 0.f, 0.f) : sphere_normal(hr, r);
+                hr.su = atan2_p(sn.x, sn.z) / (2.f * VR_PI) + 0.5f;
+                hr.sv = sn.y * 0.5f + 0.5f;
+            }
+            hr.t = dist; hr.kind = HK_EXAMPLE; hr.idx = 0;
+        }
+        return false;
+    }
+    return HAS(F_MESH);
+}
+
+// intersectScene: closest hit, attributes deferred (fill_hit).
+template <int STACK, bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
+{
+    const bool mesh = intersect_spheres<COUNT, FEAT>(p, r, hr, cnt);
+    if (mesh) {
+        traverse_mesh<STACK, COUNT, FEAT>(p, r, hr, L, cnt);
+    }
+    return hr.t < 1e20f;
+}
+
+// Materialise vHitData for the final hit (the values the reference's last
+// accepted hit wrote; :160-168, :180-189, :198-266, :380-453).
+template <uint32_t FEAT>
+__device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, const HitRec& hr, Hit& h)
+{
+    h.tan = mk4(0.f, 0.f, 0.f, 0.f);
+    const bool view_brdf = HAS(F_VIEW_BRDF);
+    if (hr.kind == HK_CORNELL || hr.kind == HK_SMALL) {
+        const Sph s = hr.kind == HK_CORNELL ? cornell_sphere(hr.idx) : small_sphere(hr.idx);
+        h.hp = add4(r.o, mul4s(r.d, hr.t));
+        h.n = normalize4(sub4(h.hp, mk4(s.px, s.py, s.pz, 0.f)));
+        h.col = mk4(s.cr, s.cg, s.cb, 0.f);
+        h.em = mk4(s.ex, s.ey, s.ez, 0.f);
+        h.type = (unsigned)s.refl;
+        h.spec = hr.kind == HK_CORNELL ? mk4(0.f, 0.f, 0.f, 0.f) : mk4(1.f, 1.f, 1.f, 0.f);
+    } else if (hr.kind == HK_EXAMPLE) {
+        const Sph s = example_sphere();
+        h.hp = add4(r.o, mul4s(r.d, hr.t));
+        if (HAS(F_TEX_DIFF) && !view_brdf)
+            h.col = p.tex[0][tex_addr(p.tex_w[0], p.tex_h[0], hr.su, hr.sv)];
+        else
+            h.col = mk4(s.cr, s.cg, s.cb, 0.f);
+        if HAS(F_TEX_NORM) {
+            const int a = tex_addr(p.tex_w[1], p.tex_h[1], hr.su, hr.sv);
+            vr4 normal = normalize4(sub4(h.hp, mk4(s.px, s.py, s.pz, 0.f)));
+            normal.w = 0.f;
+            const float rr = __builtin_sqrtf(dot4(h.hp, h.hp));
+            const float theta = acos_p(h.hp.z / rr);
+            const float phi = atan2_p(h.hp.y, h.hp.x);
+            float st, ct, sph, cph;
+            sincos_p(theta, &st, &ct);
+            sincos_p(phi, &sph, &cph);
+            h.tan = mk4(st * cph, st * sph, ct, 0.f);
+            const vr4 bitangent = cross4(normal, h.tan);
+            const vr4 nm = normalize4(sub4(muls4(2.f, p.tex[1][a]), mk4(1.f, 1.f, 1.f, 0.f)));
+            h.n = normalize4(tbn_mul(h.tan, bitangent, normal, nm));
+        } else {
+            h.n = normalize4(sub4(h.hp, mk4(s.px, s.py, s.pz, 0.f)));
+        }
+        if (HAS(F_TEX_SPEC) && !view_brdf)
+            h.spec = p.tex[2][tex_addr(p.tex_w[2], p.tex_h[2], hr.su, hr.sv)];
+        else
+            h.spec = mk4(0.f, 0.f, 0.f, 0.f);
+        h.em = mk4(0.f, 0.f, 0.f, 0.f);
+        h.type = view_brdf ? 2u : 1u;
+    } else {   // HK_MESH
+        const int a = hr.idx;
+        h.hp = add4(r.o, mul4s(r.d, hr.t));
+        const float b0 = 1.f - hr.bu - hr.bv;
+        const vr2 uv0 = p.uvs[a], uv1 = p.uvs[a + 1], uv2 = p.uvs[a + 2];
+        const float uvx = (b0 * uv0.x + hr.bu * uv1.x) + hr.bv * uv2.x;
+        const float uvy = (b0 * uv0.y + hr.bu * uv1.y) + hr.bv * uv2.y;
+        vr4 tangent = normalize4(add4(add4(muls4(b0, p.tangents[a]), muls4(hr.bu, p.tangents[a + 1])),
+                                      muls4(hr.bv, p.tangents[a + 2])));
+        tangent.w = 0.f;
+        if (HAS(F_TEX_DIFF) && !view_brdf)
+            h.col = p.tex[0][tex_addr(p.tex_w[0], p.tex_h[0], uvx, uvy)];
+        else
+            h.col = mk4(1.f, 1.f, 1.f, 0.f);
+        if (HAS(F_TEX_NORM) && dot4(tangent, tangent) > VR_EPS) {
+            const int ta = tex_addr(p.tex_w[1], p.tex_h[1], uvx, uvy);
+            vr4 normal = normalize4(add4(add4(muls4(b0, p.normals[a]), muls4(hr.bu, p.normals[a + 1])),
+                                         muls4(hr.bv, p.normals[a + 2])));
+            normal.w = 0.f;
+            const vr4 bitangent = cross4(normal, tangent);
+            const vr4 nm = normalize4(sub4(muls4(2.f, p.tex[1][ta]), mk4(1.f, 1.f, 1.f, 0.f)));
+            h.n = normalize4(tbn_mul(tangent, bitangent, normal, nm));
+        } else {
+            const vr3 a0 = p.verts[a], a1 = p.verts[a + 1], a2 = p.verts[a + 2];
+            const vr4 v0 = mk4(a0.x, a0.y, a0.z, 0.f), v1 = mk4(a1.x, a1.y, a1.z, 0.f), v2 = mk4(a2.x, a2.y, a2.z, 0.f);
+            h.n = normalize4(cross4(sub4(v0, v1), sub4(v0, v2)));
+        }
+        if (HAS(F_TEX_SPEC) && !view_brdf)
+            h.spec = p.tex[2][tex_addr(p.tex_w[2], p.tex_h[2], uvx, uvy)];
+        else
+            h.spec = mk4(0.f, 0.f, 0.f, 0.f);
+        h.tan = tangent;
+        h.em = mk4(0.f, 0.f, 0.f, 0.f);
+        h.type = view_brdf ? 2u : 1u;
+    }
+}
+
+// Emission of a hit (the only vHitData field the last bounce observes).
+__device__ __forceinline__ vr4 emission_of(const HitRec& hr) {
+    if (hr.kind == HK_CORNELL || hr.kind == HK_SMALL) {
+        const Sph s = hr.kind == HK_CORNELL ? cornell_sphere(hr.idx) : small_sphere(hr.idx);
+        return mk4(s.ex, s.ey, s.ez, 0.f);
+    }
+    return mk4(0.f, 0.f, 0.f, 0.f);
+}
+
+// MERL index maps (PathTracer.cu:473-506)
+__device__ __forceinline__ int phi_diff_index(float phi_diff) {
+    if (phi_diff < 0.0) phi_diff = (float)((double)phi_diff + 3.14159265358979323846);
+    return (int)clampi(d2i((double)phi_diff * (1.0 / (double)VR_PI * (360 / 2))), 0, 360 / 2 - 1);
+}
+__device__ __forceinline__ int theta_half_index(float theta_half) {
+    if (theta_half <= 0.0) return 0;
+    const float s = __builtin_sqrtf((float)((double)theta_half * (2.0 / (double)VR_PI)));
+    return (int)clampi(f2i(s * 90), 0, 90 - 1);
+}
+__device__ __forceinline__ int theta_diff_index(float theta_diff) {
+    return (int)clampi(d2i((double)theta_diff * (2.0 / (double)VR_PI * 90)), 0, 90 - 1);
+}
+
+// lookupBRDF (PathTracer.cu:519-566)
+__device__ __forceinline__ vr4 lookup_brdf(const float* __restrict__ T, vr4 refl, vr4 cur, vr4 normal, vr4 tangent) {
+    const vr4 bitangent = cross4(normal, tangent);
+    const vr4 H = normalize4(sub4(refl, cur));
+    float theta_H = acos_p(clampf(dot4(normal, H), 0.f, 1.f));
+    const float theta_diff = acos_p(clampf(dot4(H, refl), 0.f, 1.f));
+    float phi_diff = 0.f;
+    if ((double)theta_diff < 1e-3) {
+        phi_diff = atan2_p(clampf(-dot4(refl, bitangent), -1.f, 1.f), clampf(dot4(refl, tangent), -1.f, 1.f));
+    } else if ((double)theta_H > 1e-3) {
+        const vr4 u = muls4(-1.f, normalize4(sub4(normal, muls4(dot4(normal, H), H))));
+        const vr4 v = cross4(H, u);
+        phi_diff = atan2_p(clampf(dot4(refl, v), -1.f, 1.f), clampf(dot4(refl, u), -1.f, 1.f));
+    } else {
+        theta_H = 0.f;
+    }
+    const int ind = phi_diff_index(phi_diff) + theta_diff_index(theta_diff) * 360 / 2
+                    + theta_half_index(theta_H) * 360 / 2 * 90;
+    return mk4((float)((double)T[ind] * (1.0 / 1500.0)),
+               (float)((double)T[ind + 1458000] * (1.15 / 1500.0)),
+               (float)((double)T[ind + 2916000] * (1.66 / 1500.0)), 0.f);
+}
+
+// thrust::minstd_rand + uniform_real_distribution<float>(0,1) (rocThrust
+// random/detail/{linear_congruential_engine.inl,mod.h,uniform_real_distribution.inl})
+struct Rng {
+    uint32_t x;
+    __device__ __forceinline__ void seed(uint32_t s) {
+        uint32_t v = s >= 2147483647u ? s - 2147483647u : s;    // s % (2^31-1) for s < 2^32
+        v = v >= 2147483647u ? v - 2147483647u : v;
+        x = v ? v : 1u;
+    }
+    __device__ __forceinline__ float uniform() {
+        const uint64_t prod = (uint64_t)x * 48271u;             // Mersenne-prime reduction
+        uint32_t r = (uint32_t)(prod & 0x7fffffffu) + (uint32_t)(prod >> 31);
+        r = r >= 2147483647u ? r - 2147483647u : r;
+        x = r;
+        return (float)(r - 1u) * 4.656612873077392578125e-10f;  // / 2^31 (exact)
+    }
+};
+
+__device__ __forceinline__ uint32_t hash_seeds(uint32_t& s0, uint32_t& s1) {   // PathTracer.cu:574-580
+    s0 = 36969u * (s0 & 65535u) + (s0 >> 16);
+    s1 = 18000u * (s1 & 65535u) + (s1 >> 16);
+    return s0 * s1;
+}
+
+// trace (PathTracer.cu:597-770)
+// State of one path between bounces (trace, PathTracer.cu:597-770).
+struct PathState {
+    vr4 accum, mask;
+    float depth;
+    int bounce;
+    Rng rng;
+};
+
+// trace's prologue (:603-622); s0, s1 are updated as the reference's seeds
+__device__ __forceinline__ void path_begin(PathState& ps, uint32_t& s0, uint32_t& s1) {
+    ps.accum = mk4(0.f, 0.f, 0.f, 0.f);
+    ps.mask = mk4(1.f, 1.f, 1.f, 0.f);
+    ps.depth = 1.f;
+    ps.bounce = 0;
+    ps.rng.seed(hash_seeds(s0, s1));
+}
+
+// One bounce of trace's loop body (:627-769) for the closest hit `hr` of
+// `ray` (hr.t == 1e20: miss).  Returns true when the path ends, with its
+// radiance (w = depth) in `out`; otherwise `ray` is the next bounce's ray.
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, const HitRec& hr, PathState& ps,
+                                            vr4& out, Cnt& cnt)
+{
+    const bool hit = hr.t < 1e20f;
+    if (!hit) {
+        if (!HAS(F_CORNELL)) {                                    // :631-648
+            float lx = atan2_p(ray.d.x, ray.d.z);
+            float ly = acos_p(ray.d.y);
+            lx = lx < 0 ? (float)((double)lx + 2.0 * (double)VR_PI) : lx;
+            lx = (float)((double)lx / (2.0 * (double)VR_PI));
+            ly = ly / VR_PI;
+            const int x = f2i(lx * (float)p.hdr_w);
+            const int y = f2i(ly * (float)p.hdr_h);
+            const int val = (int)((uint32_t)x + (uint32_t)y * p.hdr_w);
+            const int addr = (int)clampi(val, 0, (int)(p.hdr_w * p.hdr_h - 1u));
+            if (COUNT) { cnt.hdr++; cnt.ld128++; }
+            ps.accum = add4(ps.accum, mul4(mul4s(ps.mask, 2.f), p.hdr[addr]));
+            ps.accum.w = ps.depth;
+            out = ps.accum;
+            return true;
+        }
+        // Cornell escape (:649-650): radiance and .w are 0.  The x channel
+        // is -0.0 -- equal to +0 in every sum it enters (a running sum that
+        // starts at +0 under round-to-nearest is never -0, so adding -0 or +0
+        // leaves its bits unchanged) -- and marks the escape in the
+        // path-result scratch, which does not store .w (store_path).
+        out = mk4(-0.f, 0.f, 0.f, 0.f);
+        return true;
+    }
+    if (!ref_alg<COUNT, FEAT>() && ps.bounce == 3) {
+        // last bounce: only the emission term is observable; the material
+        // branch below would only prepare a ray that is never traced
+        ps.accum = add4(ps.accum, mul4(ps.mask, emission_of(hr)));
+        ps.accum.w = ps.depth;
+        out = ps.accum;
+        return true;
+    }
+    Hit h;
+    fill_hit<FEAT>(p, ray, hr, h);
+    if (COUNT) {
+        if (hr.kind == HK_MESH) {
+            cnt.attr += 24 + 48;
+            cnt.mesh_hits++;
+            const bool vb = HAS(F_VIEW_BRDF);
+            const uint32_t nt = (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb);
+            cnt.tex += nt;
+            cnt.ld128 += nt;
+            // the kernel specialised on the scene's features loads the uvs
+            // only when a texture is bound and the tangents only for a normal
+            // map or a BRDF (the generic kernel counting here loads both)
+            if ((p.flags & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u) cnt.ld64 += 3;
+            if ((p.flags & (F_TEX_NORM | F_BRDF)) != 0u) cnt.ld128 += 3;
+            if (HAS(F_TEX_NORM) && dot4(h.tan, h.tan) > VR_EPS) {
+                cnt.attr += 48; cnt.tex++; cnt.nmap_hits++;
+                cnt.ld128 += 3 + 1;                            // normals + the normal-map texel
+            } else if (!ref_alg<COUNT, FEAT>()) {
+                cnt.attr += 36;     // the face normal's vertices (the reference has them from its triangle test)
+                cnt.ld96 += 3;
+            }
+        } else if (hr.kind == HK_EXAMPLE) {
+            const bool vb = HAS(F_VIEW_BRDF);
+            const uint32_t nt = (HAS(F_TEX_DIFF) && !vb) + (HAS(F_TEX_SPEC) && !vb) + (HAS(F_TEX_NORM) != 0);
+            cnt.tex += nt;
+            cnt.ld128 += nt;
+        }
+    }
+    if (ps.bounce == 0) {
+        const vr4 l = sub4(ray.o, h.hp);
+        ps.depth = sqrt_exact(dot4(l, l)) / 150.f;
+    }
+    ps.accum = add4(ps.accum, mul4(ps.mask, h.em));
+    ray.o = h.hp;
+    const vr4 normal = h.n;
+    if (h.type == 0) {                                                   // :671-676
+        ray.d = sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d)));
+        ray.o = add4(ray.o, mul4s(normal, 0.05f));
+    } else if (h.type == 1) {                                            // :678-722
+        const float aoi = dot4(h.n, muls4(-1.f, ray.d));
+        // powf only matters when spec.x != 0: X * 0 == 0 for finite X and
+        // NaN * 0 compares false, so u < fe is false either way.
+        float fe = 0.f;
+        if (h.spec.x != 0.f)
+            fe = ((1.f - p.fresnel_coef) * pow_p(1.f - aoi, p.fresnel_pow) + p.fresnel_coef * 1.f) * h.spec.x;
+        const bool reflect = (ps.rng.uniform() < fe);
+        vr4 newdir;
+        const vr4 w = normal;
+        const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
+        if (reflect) {
+            muleq4(ps.mask, h.spec);
+            newdir = normalize4(sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d))));
+        } else {
+            float rand1 = 2.f * VR_PI * ps.rng.uniform();
+            float rand2 = ps.rng.uniform();
+            const float rand2s = sqrt_exact(rand2);
+            const vr4 u = normalize4(cross4(axis, w));
+            const vr4 v = cross4(w, u);
+            float sn, cs;
+            sincos_p(rand1, &sn, &cs);
+            newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
+                                     mul4s(w, sqrt_exact(1 - rand2))));
+            muleq4(ps.mask, h.col);
+            muleq4s(ps.mask, dot4(newdir, normal));
+            muleq4s(ps.mask, 2.f);
+        }
+        ray.o = add4(ray.o, mul4s(normal, 0.05f));
+        ray.d = newdir;
+    } else if (h.type == 2) {                                            // :724-764
+        const vr4 w = normal;
+        const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
+        float rand1 = 2.f * VR_PI * ps.rng.uniform();
+        float rand2 = ps.rng.uniform();
+        const float rand2s = sqrt_exact(rand2);
+        const vr4 u = normalize4(cross4(axis, w));
+        const vr4 v = cross4(w, u);
+        float sn, cs;
+        sincos_p(rand1, &sn, &cs);
+        const vr4 newdir = normalize4(add4(add4(mul4s(mul4s(u, cs), rand2s), mul4s(mul4s(v, sn), rand2s)),
+                                           mul4s(w, sqrt_exact(1 - rand2))));
+        if HAS(F_BRDF) {
+            const float dw = 24 * pow_p(newdir.x * newdir.x + newdir.y * newdir.y + newdir.z * newdir.z, -1.5f);
+            if (COUNT) { cnt.brdf++; cnt.ld32 += 3; }
+            const vr4 b = lookup_brdf(p.brdf, newdir, ray.d, h.n, h.tan);
+            const vr4 bm = mk4(__builtin_fmaxf(b.x, 0.f), __builtin_fmaxf(b.y, 0.f), __builtin_fmaxf(b.z, 0.f),
+                               __builtin_fmaxf(b.w, 0.f));
+            muleq4(ps.mask, muls4(dw, bm));
+        } else {
+            muleq4(ps.mask, h.col);
+            muleq4s(ps.mask, dot4(newdir, normal));
+            muleq4s(ps.mask, 2.f);
+        }
+        ray.o = add4(ray.o, mul4s(normal, 0.05f));
+        ray.d = newdir;
+    }
+    if (++ps.bounce == 4) {
+        ps.accum.w = ps.depth;
+        out = ps.accum;
+        return true;
+    }
+    return false;
+}
+
+template <int STACK, bool COUNT, uint32_t FEAT>
+__device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit0, uint32_t& s0, uint32_t& s1,
+                     const Lds& L, Cnt& cnt, float& depth)
+{
+    PathState ps;
+    path_begin(ps, s0, s1);
+    for (;;) {
+        HitRec hr;
+        if (!ref_alg<COUNT, FEAT>() && ps.bounce == 0) {
+            // the camera ray is the same for both samples of every frame (no
+            // jitter, PathTracer.cu:842-844): its hit is computed once per pixel
+            hr = hr0;
+            (void)hit0;
+        } else {
+            (void)intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, L, cnt);
+        }
+        vr4 out;
+        if (bounce_step<COUNT, FEAT>(p, ray, hr, ps, out, cnt)) { depth = ps.depth; return out; }
+    }
+}
+
+// colour of the accumulated radiance after `frame` frames (PathTracer.cu:850-866)
+__device__ __forceinline__ u8x4 tonemap(vr4 io, uint32_t frame) {
+    const float coef = 1.f / (float)frame;
+    const vr4 sc = mul4s(io, coef);
+    const float inv_gamma = 1.f / 2.2f;
+    u8x4 c;
+    c.x = f2u8(pow_p(clampf(sc.x, 0.f, 1.f), inv_gamma) * 255);
+    c.y = f2u8(pow_p(clampf(sc.y, 0.f, 1.f), inv_gamma) * 255);
+    c.z = f2u8(pow_p(clampf(sc.z, 0.f, 1.f), inv_gamma) * 255);
+    c.w = 0xff;
+    return c;
+}
+
+// A path's result in the scratch (RenderParams::paths): its radiance, 12 B.
+// The .w bounce_step returns is the primary hit's depth term (ps.depth, set
+// at bounce 0, the same for every path of a pixel: no camera jitter) on
+// every exit but a Cornell escape, which returns 0 and marks itself with
+// x = -0.0.  So .w is not stored per path: path 0 of the pixel stores the
+// depth term once (path_w) and finish_kernel rebuilds each path's .w from
+// it and the escape mark -- a quarter less scratch written by the path
+// kernel and read by the (HBM-bound) finish pass.
+__device__ __forceinline__ bool escaped(float x) { return __float_as_uint(x) == 0x80000000u; }
+__device__ __forceinline__ void store_path(const RenderParams& p, uint32_t q, uint32_t slot, const vr4& out, float depth)
+{
+    p.paths[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
+    if (q == 0u) p.path_w[slot] = depth;
+}
+
+// Binds this thread's stack column and fills the block's node cache with
+// the first nodes of the area-ordered node array.
+template <uint32_t FEAT, int BT = kBlockThreads>
+__device__ __forceinline__ Lds lds_setup(const RenderParams& p, int* lds_stack, vr4* lds_nodes, int2* lds_idx,
+                                         int cn, int tid)
+{
+    Lds L;
+    L.stk = lds_stack + tid;
+    L.stride = BT;
+    L.nodes = lds_nodes;
+    L.idx = lds_idx;
+    L.n_cached = 0;
+    if (HAS(F_MESH)) {
+        if (!HAS(F_STRICT)) {            // fp16 nodes, 32 B: 1.5x as many fit
+            const uint32_t cap = (uint32_t)(3 * cn / 2);
+            L.n_cached = (int)(p.n_nodes < cap ? p.n_nodes : cap);
+            for (int i = tid; i < 2 * L.n_cached; i += BT) lds_nodes[i] = p.bvh16[i];
+        } else {
+            L.n_cached = (int)(p.n_nodes < (uint32_t)cn ? p.n_nodes : (uint32_t)cn);
+            for (int i = tid; i < 3 * L.n_cached; i += BT) lds_nodes[i] = p.bvh[(i / 3) * 4 + i % 3];
+            for (int i = tid; i < L.n_cached; i += BT)
+                lds_idx[i] = *reinterpret_cast<const int2*>(p.bvh + 4 * i + 3);
+        }
+        __syncthreads();
+    }
+    return L;
+}
+
+// Camera ray through pixel (x, y) (PathTracer.cu:842-844: no jitter).
+__device__ __forceinline__ Ray camera_ray(const RenderParams& p, uint32_t x, uint32_t y)
+{
+    // (float)((0.25 + x) / W - 0.5) and the same for y, evaluated in double
+    // on the host once per column / row (vrhip_create)
+    const float sx = p.cam_sxy[x];
+    const float sy = p.cam_sxy[p.W + y];
+    Ray cam;
+    cam.o = p.cam_o;
+    cam.d = normalize4(add4(add4(p.cam_d, mul4s(p.cx, sx)), mul4s(p.cy, sy)));
+    return cam;
+}
+
+// render (PathTracer.cu:791-868), K frames per launch.
+#ifndef VR_MIN_WAVES_PER_SIMD
+#define VR_MIN_WAVES_PER_SIMD 4
+#endif
+// 64-entry stacks take 64 KiB of LDS per 256 threads: at most 2 waves/SIMD
+constexpr int min_waves(int stack) { return stack > 32 ? 2 : VR_MIN_WAVES_PER_SIMD; }
+template <int STACK, bool COUNT, uint32_t FEAT>
+__global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel(const RenderParams p)
+{
+    constexpr int CN = cache_nodes(STACK);
+    __shared__ int lds_stack[STACK * kBlockThreads];
+    __shared__ vr4 lds_nodes[3 * CN];
+    __shared__ int2 lds_idx[CN];
+    const int tid = threadIdx.x;
+    const Lds L = lds_setup<FEAT>(p, lds_stack, lds_nodes, lds_idx, CN, tid);
+    // block -> (tile, path group): the 2*n_frames paths of a pixel are split
+    // into p.split contiguous groups run by different blocks (strong-scaling
+    // and tail balance); group g of tile t is block t*split + g
+    const uint32_t T = p.split;
+    const uint32_t tile = blockIdx.x / T;
+    const uint32_t g = blockIdx.x - tile * T;
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
+    const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
+    if (x >= p.wr || y >= p.hr) return;   // never true for a valid launch
+    Cnt cnt;
+
+    const uint32_t ind = x + y * p.W;
+    const Ray cam = camera_ray(p, x, y);
+    HitRec hr0;
+    bool hit0 = false;
+    if (!ref_alg<COUNT, FEAT>()) hit0 = intersect_scene<STACK, COUNT, FEAT>(p, cam, hr0, L, cnt);
+
+    // path q = 2*f + s (frame f of the launch, sample s); the seeds of a
+    // frame's second sample are its first sample's after one hash (:620-622)
+    const uint32_t n_paths = 2u * p.n_frames;
+    const uint32_t chunk = (n_paths + T - 1u) / T;
+    const uint32_t q0 = g * chunk;
+    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
+    const bool direct = !p.use_scratch;                  // accumulate here (counting launches)
+    vr4 io = (direct && p.first_frame != 1u) ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
+    uint32_t s1 = 0, s2 = 0;
+    float last_w = 0.f;
+#pragma unroll 1
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t f = q >> 1;
+        if ((q & 1u) == 0u || q == q0) {
+            s1 = x * (p.first_frame + f);
+            s2 = y * p.times[f];
+            if (q & 1u) (void)hash_seeds(s1, s2);
+        }
+        float depth;
+        const vr4 result = trace<STACK, COUNT, FEAT>(p, cam, hr0, hit0, s1, s2, L, cnt, depth);
+        if (direct)
+            io = add4(io, mul4s(result, 1.f / 2.f));
+        else
+            store_path(p, q, tile * kBlockThreads + (uint32_t)tid, result, depth);
+        last_w = result.w;
+    }
+    if (direct) {   // else finish_kernel accumulates the paths' results in path order
+        // only the launch's last frame is observable in the colour and depth
+        // surfaces (each frame of the reference overwrites them, :846-866)
+        const unsigned char db = f2u8((1.f - last_w) * 255);
+        u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
+        p.depth[ind] = dv;
+        p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
+        p.accum[ind] = io;
+    }
+    if (COUNT) flush_counts(p, cnt, lane, (FEAT & F_COUNT_EXEC) != 0u);
+}
+
+// Kernels without the example sphere (whose hits need the u,v slots) store
+// the camera ray's direction in the primary record instead, so a path starts
+// without recomputing it (two f64 divisions and a normalisation).
+template <uint32_t FEAT>
+constexpr bool prim_has_dir() { return (FEAT & F_EXAMPLE) == 0; }
+
+// Primary hits, one thread per owned pixel: the camera ray's closest hit
+// (the HitRec intersect_scene returns: t, kind, idx, barycentrics,
+// example-sphere u,v), two float4s per pixel in the scratch order of
+// p.paths, read by every path of the pixel in render_wave_kernel.  One ray
+// per thread, so no LDS node cache.
+template <int STACK, uint32_t FEAT>
+__global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderParams p)
+{
+    __shared__ int lds_stack[STACK * kBlockThreads];
+    const int tid = threadIdx.x;
+    Lds L;
+    L.stk = lds_stack + tid;
+    L.stride = kBlockThreads;
+    L.nodes = nullptr;
+    L.idx = nullptr;
+    L.n_cached = 0;
+    const uint32_t tile = blockIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
+    const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
+    constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;
+    Cnt cnt;
+    HitRec hr;
+    const Ray cam = camera_ray(p, x, y);
+    (void)intersect_scene<STACK, CNT, FEAT>(p, cam, hr, L, cnt);
+    vr4* dst = p.prim + 2u * ((size_t)tile * kBlockThreads + tid);
+    dst[0] = mk4(hr.t, __int_as_float(hr.kind), __int_as_float(hr.idx), hr.bu);
+    if constexpr (prim_has_dir<FEAT>())
+        dst[1] = mk4(hr.bv, cam.d.x, cam.d.y, cam.d.z);   // the paths reuse the camera ray too
+    else
+        dst[1] = mk4(hr.bv, hr.su, hr.sv, 0.f);
+    if (CNT) flush_counts(p, cnt, lane, true);
+}
+
+// Path-pool render (the default for mesh scenes), a persistent kernel over
+// work queues.  The launch's paths are cut into chunks of 64 items: chunk =
+// (sub-tile s, path q), s an 8x8 quadrant of one of the rank's tiles, item i
+// = pixel i of s.  The grid is one resident wave set; each wave takes chunks
+// from the queues and its lanes run one path each through a small state
+// machine (setup = sphere tests, traverse the mesh, shade).  A lane whose path
+// ends stores the radiance to p.paths[q][pixel] and takes the next item
+// (ballot + mbcnt give each idle lane its item in one wave-uniform step), so
+// lanes whose rays finish early do not idle while the wave's other lanes
+// traverse, and no wave waits at the end of the launch for blocks of uneven
+// cost.  Traversal pauses between outer iterations (trav_iter) once
+// VR_SHADE_BATCH lanes wait for shading.
+//
+// Primary hits: the camera ray is the same for every path of a pixel (no
+// jitter, PathTracer.cu:842-844), so primary_kernel traces it once per pixel
+// per launch and every path of the pixel starts at its shading.  Launches of
+// one frame (2 paths per pixel, the reference's render() cadence) skip that
+// serial pass (RenderParams::inline_prim): each path traces its camera ray in
+// the pool, where the primary pass's latency tail overlaps other lanes' work.
+//
+// Every path runs exactly the operations of trace(); only the interleaving
+// of paths on the SIMD changes, so results are bit-identical.
+// finish_kernel then sums each pixel's paths in path order.
+#ifndef VR_SHADE_BATCH
+#define VR_SHADE_BATCH 16
+#endif
+#ifndef VR_SHADE_RATIO
+#define VR_SHADE_RATIO 1
+#endif
+// Once the queues are drained, the paths waiting to be shaded are shaded
+// together once n_shade * VR_DRAIN_SHADE_NUM >= n_trav * VR_DRAIN_SHADE_DEN
+// (or no lane traverses): each shading round costs the wave a whole pass
+// through the shading code, and in the drain the traversing lanes' paths --
+// the launch's longest -- wait through every such round.  Measured (r03o,
+// one frame per call; 8-rank shard steps): shading at the first waiting
+// path C3 0.504 / C2 0.765 ms, 0.631 / 1.333 ms; at n_shade >= n_trav 0.470 /
+// 0.731, 0.612 / 1.343; at 2 n_shade >= n_trav 0.476 / 0.740.
+#ifndef VR_DRAIN_SHADE_NUM
+#define VR_DRAIN_SHADE_NUM 1
+#endif
+#ifndef VR_DRAIN_SHADE_DEN
+#define VR_DRAIN_SHADE_DEN 1
+#endif
+enum LaneState : int { LS_SETUP = 0, LS_TRAV = 1, LS_SHADE = 2, LS_DONE = 3, LS_CAMERA = 4, LS_HELP = 5, LS_HELPDONE = 6 };
+
+// Helpers (the launch's drain).  Once the work queues are empty, a wave's
+// lanes idle as their paths end while a few lanes still walk long
+// traversals -- the paths that end the launch.  Then an idle lane takes the
+// top entry of a traversing lane's stack (a subtree or a leaf the owner
+// would visit next), walks it with the owner's ray, its closest hit so far
+// and its culling distance, and hands its closest hit back; the owner shades
+// once its own walk and all its helpers' are done.  The closest hit does not
+// depend on the order in which subtrees are visited: a triangle at exactly
+// the closest distance is resolved by the reference's own order (ref_first),
+// so the merged hit is the reference's.  Not used by the strict walk, whose
+// exact result relies on the reference's visit order.
+#ifndef VR_HELPERS
+#define VR_HELPERS 1
+#endif
+template <uint32_t FEAT>
+constexpr bool helpers() { return VR_HELPERS != 0 && (FEAT & F_STRICT) == 0u && (FEAT & F_SMALL) != 0u; }
+
+// One wave-synchronous help round: (1) finished helpers hand their closest
+// hit to their owners, one at a time; (2) idle lanes take a subtree each from
+// traversing lanes (one per owner per round, pairing the k-th idle lane with
+// the k-th owner).  For helpers `slot` holds the owner's lane.
+__device__ __forceinline__ uint32_t help_step(const RenderParams& p, int lane, int& state, int& pend, uint32_t& slot,
+                                              Ray& ray, Trav& tr, const Lds& L)
+{
+    unsigned long long hd = __ballot(state == LS_HELPDONE);
+    while (hd != 0ull) {
+        const int h = __ffsll((long long)hd) - 1;
+        hd &= hd - 1ull;
+        const int o = __builtin_amdgcn_readlane((int)slot, h);
+        const float ht = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tr.t), h));
+        const int hb = __builtin_amdgcn_readlane(tr.best, h);
+        const float hu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tr.bu), h));
+        const float hv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tr.bv), h));
+        if (lane == o) {
+            // the helper started from this lane's closest hit at the hand-out:
+            // it returns that one, a closer one, or a tie it resolved
+            const bool closer = hb >= 0 && (ht < tr.t || (ht == tr.t && hb != tr.best &&
+                                                          (tr.best < 0 || ref_first(p, tr, hb / 3, tr.best / 3))));
+            if (closer) {
+                tr.t = ht; tr.best = hb; tr.bu = hu; tr.bv = hv;
+                tr.tcull = tr.t * 1.0009765625f;
+            }
+            --pend;
+        }
+        if (lane == h) state = LS_DONE;
+    }
+    // helpers cull with the owner's closest hit as it improves
+    const int own = state == LS_HELP ? (int)slot : lane;
+    const float ot = __shfl(tr.t, own, 64);
+    if (state == LS_HELP) tr.tcull = __builtin_fminf(tr.tcull, ot * 1.0009765625f);
+    const bool idle = state == LS_DONE;
+    const bool can = state == LS_TRAV && tr.nodeAddr != kSentinel && tr.sp >= 1;
+    const unsigned long long im = __ballot(idle), cm = __ballot(can);
+    if (im == 0ull || cm == 0ull) return 0u;
+    const uint32_t ni = (uint32_t)__popcll(im), nc = (uint32_t)__popcll(cm), n = ni < nc ? ni : nc;
+    const uint32_t rc = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+    const uint32_t ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+    int give = 0;
+    if (can && rc < n) {                                   // the owner hands out its next stack entry
+        give = L.stk[tr.sp * L.stride];
+        tr.sp--;
+        ++pend;
+    }
+    int src = lane;                                        // idle lane ri takes the ri-th owner
+    unsigned long long m = cm;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int ol = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        if (idle && ri == k) src = ol;
+    }
+    const bool take = idle && ri < n;
+    const int e = __shfl(give, src, 64);
+    auto pull = [&](float& v) { v = __shfl(v, src, 64); };
+    pull(ray.o.x); pull(ray.o.y); pull(ray.o.z); pull(ray.o.w);
+    pull(ray.d.x); pull(ray.d.y); pull(ray.d.z); pull(ray.d.w);
+    pull(tr.ivx); pull(tr.ivy); pull(tr.ivz); pull(tr.odx); pull(tr.ody); pull(tr.odz);
+    pull(tr.t); pull(tr.tcull); pull(tr.bu); pull(tr.bv);
+    tr.best = __shfl(tr.best, src, 64);
+    if (take) {
+        state = LS_HELP;
+        slot = (uint32_t)src;
+        tr.sp = 0;
+        L.stk[0] = kSentinel;
+        tr.nodeAddr = e;
+    }
+    return n;                                              // subtrees handed out this round
+}
+// Age-based wave priority (s_setprio) in the path kernel, thresholds in us:
+// VR_AGE_PRIO 1 in every path kernel, 2 in the one-frame kernels only
+// (F_INLINE_PRIM: the reference's render() cadence, where a launch ends on
+// its oldest paths), 0 off.  Measured (r03e, 1xMI355X): one frame per call
+// C2 0.840 -> 0.799 ms, C3 0.564 -> 0.570 (noise); 16-frame launches C2
+// -0.4 %, C3 -0.1 %.
+#ifndef VR_AGE_PRIO
+#define VR_AGE_PRIO 2
+#endif
+template <uint32_t FEAT>
+constexpr bool age_prio() { return VR_AGE_PRIO == 1 || (VR_AGE_PRIO == 2 && (FEAT & F_INLINE_PRIM) != 0u); }
+#ifndef VR_AGE_T1
+#define VR_AGE_T1 100
+#endif
+#ifndef VR_AGE_T2
+#define VR_AGE_T2 200
+#endif
+#ifndef VR_AGE_T3
+#define VR_AGE_T3 300
+#endif
+
+
+// Block size of the path kernel: its blocks hold no tiles, so one block of
+// 1,024 threads per CU shares one LDS node cache four times the size of a
+// 256-thread block's (at the same 4 waves/SIMD).
+// Path-kernel residency by stack size: with 16- and 24-entry stacks (C2, C3;
+// C5) VR_PATH_WAVES waves per SIMD in VR_PATH_BLOCK-thread blocks; 32-entry
+// stacks 4 waves in one 1,024-thread block per CU (the stacks alone take
+// 128 KB); 64-entry stacks 2 waves in 256-thread blocks.  Measured (C2 / C3,
+// no packed f32): 4 waves in 1,024 threads 3,029 / 10,724; 5 in 256: 2,956 /
+// 10,503; 6 in 256: 3,228 / 11,352; 6 in 512: 2,952 / 10,483; 6 in 768:
+// 3,406 / 12,193; 7 in 256 (spills): 3,317 / 11,290.
+#ifndef VR_PATH_WAVES
+#define VR_PATH_WAVES 6
+#endif
+#ifndef VR_PATH_BLOCK
+#define VR_PATH_BLOCK 768
+#endif
+static_assert(VR_PATH_BLOCK % kBlockThreads == 0, "VR_PATH_BLOCK must be a multiple of 256");
+static_assert((4 * VR_PATH_WAVES * 64) % VR_PATH_BLOCK == 0, "whole blocks per CU");
+// Cornell-box mesh kernels with 16-entry stacks (C2) run 7 waves per SIMD in
+// 256-thread blocks (72 VGPRs, SGPR spills only): C2 3,991 -> 4,109 Mpaths/s,
+// while the HDRI scenes lose with it (C3 -2 %, C5 -17 %: their longer shading
+// code spills) and keep VR_PATH_WAVES in VR_PATH_BLOCK-thread blocks.
+#ifndef VR_PATH_WAVES_CORNELL
+#define VR_PATH_WAVES_CORNELL 7
+#endif
+#ifndef VR_PATH_BLOCK_CORNELL
+#define VR_PATH_BLOCK_CORNELL 256
+#endif
+static_assert(VR_PATH_BLOCK_CORNELL % kBlockThreads == 0, "VR_PATH_BLOCK_CORNELL must be a multiple of 256");
+static_assert((4 * VR_PATH_WAVES_CORNELL * 64) % VR_PATH_BLOCK_CORNELL == 0, "whole blocks per CU");
+// c: the kernel is a Cornell-box specialisation (cornell_kernel<FEAT>())
+constexpr bool cornell_res(int stack, bool c) { return c && stack <= 16; }
+constexpr int wave_block(int stack, bool c) {
+    return cornell_res(stack, c) ? VR_PATH_BLOCK_CORNELL : stack <= 24 ? VR_PATH_BLOCK : stack <= 32 ? 1024 : kBlockThreads;
+}
+// Launches of fewer than 2^24 paths (sharded frames, RenderParams::small_blocks)
+// take 256-thread blocks at the same residency: a block frees its CU slot once
+// its 4 waves are done rather than 12, so the launch's drain overlaps the next
+// launch sooner.  Projected 8-rank C2 step 1.283 -> 1.193 ms (C3 0.468 ->
+// 0.420 ms), while whole frames keep the 768-thread blocks (C2 3,437 vs 3,244).
+constexpr int wave_block_small(int stack, bool c) { return stack <= 24 ? kBlockThreads : wave_block(stack, c); }
+constexpr int path_waves(int stack, bool c) {
+    return cornell_res(stack, c) ? VR_PATH_WAVES_CORNELL : stack <= 24 ? VR_PATH_WAVES : stack <= 32 ? 4 : 2;
+}
+constexpr int path_blocks_per_cu(int stack, int bt, bool c) { return 4 * path_waves(stack, c) * 64 / bt; }
+// LDS per block: an equal share of the CU's 160 KB less 256 B per 256 threads;
+// the node cache takes what the stacks leave (56 B per node)
+constexpr int path_cache_nodes(int stack, int bt, bool c) {
+    return (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * 4) / 56 > 0
+               ? (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * 4) / 56 : 1;
+}
+template <uint32_t FEAT>
+constexpr bool cornell_kernel() {
+    // the one-frame kernels (F_INLINE_PRIM) keep 6 waves: at 7 the interactive
+    // C2 rate fell 2,147 -> 2,100 Mpaths/s (r02g); so do the small-launch
+    // kernels (F_SMALL), which spilled 19 VGPRs at 7 with helper lanes and
+    // cost counting (8-rank C2 shard step 1.317 -> 1.257 ms at 6, r03p)
+    return (FEAT & F_EXACT) != 0u && (FEAT & F_CORNELL) != 0u && (FEAT & F_INLINE_PRIM) == 0u &&
+           (FEAT & F_SMALL) == 0u;
+}
+
+#ifndef VR_XCD_BANDS
+#define VR_XCD_BANDS 128
+#endif
+
+template <int STACK, uint32_t FEAT, int BT>
+__device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L);
+
+// Pixel of item `px` of this rank's 8x8 sub-tile `sub` (wave-uniform in the
+// path kernel, so the tile arithmetic, a division included, stays scalar).
+__device__ __forceinline__ void sub_pixel(const RenderParams& p, uint32_t sub, uint32_t px, uint32_t& x, uint32_t& y)
+{
+    const uint32_t tile = sub >> 2, quad = sub & 3u;
+    const uint32_t gtile = p.rank + tile * p.nranks;       // tiles dealt round-robin to ranks
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    x = tile_x * 16u + (quad & 1u) * 8u + (px & 7u);
+    y = tile_y * 16u + (quad >> 1) * 8u + (px >> 3);
+}
+
+// The launch's drained-queue mask (bit q: head q has handed out its last
+// chunk), after the VR_MAX_QUEUES heads; reset with them by finish_kernel.
+__device__ __forceinline__ unsigned long long* queue_drained_mask(uint32_t* chunk_ctr)
+{
+    return reinterpret_cast<unsigned long long*>(chunk_ctr + VR_MAX_QUEUES * kQueueStride);
+}
+__device__ __forceinline__ unsigned long long all_q_of(uint32_t Q) { return Q >= 64u ? ~0ull : ((1ull << Q) - 1ull); }
+
+// The sub-tile that value v of work-queue head q hands out (>= n_sub: the
+// queue is drained; non-decreasing in v), and the path in `path`.
+// Chunk = (sub-tile, path): the paths of one sub-tile are handed out
+// together.  With VR_XCD_BANDS queue q serves XCD q % 8 (blocks b % 16 == q
+// under round-robin dispatch): bands of VR_XCD_BANDS sub-tiles are dealt
+// round-robin to the XCDs, each XCD's chunks sub-major, alternated between
+// its Q / 8 queues.
+__device__ __forceinline__ uint32_t queue_item(uint32_t q, uint32_t v, uint32_t Q, uint32_t n_paths, uint32_t& path)
+{
+#if VR_XCD_BANDS
+    const uint32_t x = q % 8u, h = q / 8u;
+    const uint32_t e = v * (Q / 8u) + h;
+    const uint32_t per_band = (uint32_t)VR_XCD_BANDS * n_paths;
+    const uint32_t g = e / per_band, o = e - g * per_band;
+    const uint32_t r = o / n_paths;
+    path = o - r * n_paths;
+    return (g * 8u + x) * (uint32_t)VR_XCD_BANDS + r;
+#else
+    const uint32_t c = v * Q + q;
+    const uint32_t sb = c / n_paths;
+    path = c - sb * n_paths;
+    return sb;
+#endif
+}
+
+template <int STACK, uint32_t FEAT, int BT>
+__global__ void __launch_bounds__(BT, path_waves(STACK, cornell_kernel<FEAT>())) render_wave_kernel(const RenderParams p)
+{
+    constexpr int CN = path_cache_nodes(STACK, BT, cornell_kernel<FEAT>());
+    __shared__ int lds_stack[STACK * BT];
+    __shared__ vr4 lds_nodes[3 * CN];
+    __shared__ int2 lds_idx[CN];
+    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_nodes, lds_idx, CN, (int)threadIdx.x);
+    wave_body<STACK, FEAT, BT>(p, L);
+}
+
+template <int STACK, uint32_t FEAT, int BT>
+__device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
+{
+    const int tid = (int)threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t n_paths = 2u * p.n_frames;
+    const uint32_t n_sub = p.path_stride >> 6;             // 8x8 sub-tiles of the rank's tiles
+    constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;      // instrumented copy (vrhip_render_profiled)
+    Cnt cnt;
+
+    // Work queues: chunk c = (sub-tile c / n_paths, path c % n_paths), so the
+    // paths of one sub-tile are handed out together (coherent rays, the
+    // sub-tile's primary records in cache).  p.n_queues heads, queue j hands
+    // out chunks j, j + Q, j + 2Q, ... (one device-scope atomic per chunk; a
+    // single head saturates: MI355X_MICROARCH "dequeue").  A wave draws from
+    // its block's queue and, once that is drained, from the following ones.
+    // With VR_XCD_BANDS (default 128 sub-tiles = 32 tiles) the sub-tiles are
+    // dealt to the 8 XCDs in bands, so each XCD's L2 serves a coherent part of
+    // the image (C2 +0.7 %, C3 +1.7 %, C5 +0.7 % over chunk-interleaved queues).
+    const uint32_t Q = p.n_queues;                         // power of two, multiple of the 8 XCDs
+    uint32_t qj = blockIdx.x & (Q - 1u);
+    // queues this wave knows to be drained (its own failed dequeues and the
+    // launch's drained-queue mask, queue_drained_mask), kept in LDS: the
+    // kernel is at its register limits and this is consulted only at the end
+    __shared__ unsigned long long lds_dead[BT / 64];
+    unsigned long long* const my_dead = lds_dead + (tid >> 6);
+    if (lane == 0) *my_dead = 0ull;
+    uint32_t drained = 0;                                  // whole-frame launches: queues found drained
+    auto grab = [&](uint32_t& sub, uint32_t& path) {       // wave-uniform; sub = ~0u when no work is left
+        for (;;) {
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(p.chunk_ctr + qj * kQueueStride, 1u);
+            const uint32_t sb = queue_item(qj, __builtin_amdgcn_readfirstlane(v), Q, n_paths, path);
+            if (sb < n_sub) {
+#if VR_XCD_BANDS
+                // longest-first: the XCD's sub-tiles in the order of the
+                // previous launch's cost (order_kernel); else band order
+                if (p.sub_order) {
+                    const uint32_t x = qj % 8u, r = sb % (uint32_t)VR_XCD_BANDS, g = sb / (8u * (uint32_t)VR_XCD_BANDS);
+                    sub = p.sub_order[x * p.order_cap + g * (uint32_t)VR_XCD_BANDS + r];
+                    return;
+                }
+#endif
+                sub = sb;
+                return;
+            }
+            // queue qj is drained.
+            if constexpr ((FEAT & F_SMALL) == 0u) {
+                // whole-frame launches (a drain of ~1 % of the launch; the
+                // 7-wave kernel has no register to spare): the next queues
+                // in turn, one failed dequeue each
+                if (++drained == Q) { sub = ~0u; path = 0; return; }
+                qj = qj + 1u == Q ? 0u : qj + 1u;
+                continue;
+            }
+            // Small launches (one frame per call, shards: the drain is a large
+            // share of them) publish a drained queue once (the first wave to
+            // see it) and skip every queue the mask holds: a wave learns that
+            // the launch is out of work from one failed dequeue and one load,
+            // instead of one failed atomic on each of the Q heads -- at the end
+            // of a launch all of its waves did that together, n_waves x Q
+            // atomics on Q words (~88 per us per word), tens of us before the
+            // grid could retire.  Every bit stands for a failed dequeue, so the
+            // wave leaves only when all queues are drained.
+            uint32_t m0 = 0, m1 = 0;
+            if (lane == 0) {
+                unsigned long long* const dmask = queue_drained_mask(p.chunk_ctr);
+                // the first failed dequeue of a queue (exactly one per queue:
+                // no storm of ORs on the mask word when many waves run dry at
+                // once) publishes it; the others read the mask with an
+                // L1-bypassing load (a stale copy only hides drained queues,
+                // which then cost a failed dequeue each, as without the mask)
+                uint32_t pth;
+                const uint32_t v0 = __builtin_amdgcn_readfirstlane(v);
+                const bool first = v0 == 0u || queue_item(qj, v0 - 1u, Q, n_paths, pth) < n_sub;
+                const unsigned long long m = first ? atomicOr(dmask, 1ull << qj)
+                                                   : __hip_atomic_load(dmask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long d = *my_dead | m | (1ull << qj);
+                *my_dead = d;
+                m0 = (uint32_t)d; m1 = (uint32_t)(d >> 32);
+            }
+            const unsigned long long live = all_q_of(Q) & ~(((unsigned long long)__builtin_amdgcn_readfirstlane(m1) << 32) |
+                                                             (unsigned long long)__builtin_amdgcn_readfirstlane(m0));
+            if (live == 0ull) { sub = ~0u; path = 0; return; }
+            const unsigned long long after = qj + 1u < 64u ? (live >> (qj + 1u)) << (qj + 1u) : 0ull;
+            qj = (uint32_t)__builtin_ctzll(after != 0ull ? after : live);
+        }
+    };
+    uint32_t cur_sub, cur_q;
+    grab(cur_sub, cur_q);                                  // wave-uniform: chunk being handed out
+    uint32_t next = 64u;                                   // items of the current chunk handed out
+    int state = LS_DONE;
+    uint32_t q = 0, slot = 0;                              // this lane's path and pixel slot
+    uint32_t cam_xy = 0;                                   // F_INLINE_PRIM: its pixel (x << 16 | y) until LS_CAMERA
+    Ray ray;
+    PathState ps;
+    HitRec hr;
+    Trav tr;
+    int pend = 0;                                          // helpers: subtrees this lane's walk handed out, not yet merged
+    uint32_t born = 0;                                     // age_prio: this lane's path start (s_memrealtime, 100 MHz)
+    uint32_t now_tick = age_prio<FEAT>() ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+    auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
+        if (sub == ~0u) { state = LS_DONE; return; }
+        q = path;
+        slot = sub * 64u + px;
+        const uint32_t f = q >> 1;
+        uint32_t x, y;
+        sub_pixel(p, sub, px, x, y);
+        uint32_t s1 = x * (p.first_frame + f);
+        uint32_t s2 = y * p.times[f];
+        if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
+        path_begin(ps, s1, s2);
+        born = now_tick;
+        if constexpr ((FEAT & F_SMALL) != 0u) cnt.work = 0;
+        if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {      // few paths per pixel: trace the camera ray here
+            cam_xy = (x << 16) | y;                        // (set up at the top of the loop, out of the refill)
+            state = LS_CAMERA;
+            return;
+        }
+        if (CNT) cnt.ld128 += 2;
+        const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
+        hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
+        hr.bv = b.x;
+        if constexpr (prim_has_dir<FEAT>()) {
+            hr.su = hr.sv = 0.f;
+            ray.o = p.cam_o;
+            ray.d = mk4(b.y, b.z, b.w, (p.cam_d.w + p.cx.w) + p.cy.w);   // camera_ray's .w
+        } else {
+            hr.su = b.y; hr.sv = b.z;
+            ray = camera_ray(p, x, y);
+        }
+        state = LS_SHADE;
+    };
+    start(cur_sub, cur_q, (uint32_t)lane);
+
+    for (;;) {
+        if constexpr (age_prio<FEAT>()) {
+            // age-based issue priority: a wave holding an old path issues
+            // ahead of the SIMD's other waves, so the longest paths -- the
+            // end of the launch -- are not also the slowest
+            now_tick = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            const uint32_t age = state != LS_DONE ? now_tick - born : 0u;
+            if (__ballot(age > (uint32_t)(VR_AGE_T3 * 100)) != 0ull) __builtin_amdgcn_s_setprio(3);
+            else if (__ballot(age > (uint32_t)(VR_AGE_T2 * 100)) != 0ull) __builtin_amdgcn_s_setprio(2);
+            else if (__ballot(age > (uint32_t)(VR_AGE_T1 * 100)) != 0ull) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {
+            if (state == LS_CAMERA) {
+                ray = camera_ray(p, cam_xy >> 16, cam_xy & 0xffffu);
+                state = LS_SETUP;
+            }
+        }
+        if (state == LS_SETUP) {
+            if (intersect_spheres<CNT, FEAT>(p, ray, hr, cnt)) {
+                trav_init<FEAT>(p, ray, hr.t, tr, L);
+                state = LS_TRAV;
+            } else {
+                state = LS_SHADE;
+            }
+        }
+        if (HAS(F_MESH)) {
+            for (;;) {
+                const int n_trav = __popcll(__ballot(state == LS_TRAV || state == LS_HELP));
+                if (n_trav == 0) break;
+                const int n_shade = __popcll(__ballot(state == LS_SHADE));
+                if (n_shade >= VR_SHADE_BATCH && n_shade * VR_SHADE_RATIO >= n_trav) break;
+                // queue drained: no lane will be refilled; shade in batches
+                if (cur_sub == ~0u && n_shade > 0 && n_shade * VR_DRAIN_SHADE_NUM >= n_trav * VR_DRAIN_SHADE_DEN)
+                    break;
+                if constexpr (helpers<FEAT>()) {
+                    if (cur_sub == ~0u || __ballot(state == LS_HELP || state == LS_HELPDONE) != 0ull)
+                        (void)help_step(p, lane, state, pend, slot, ray, tr, L);
+                }
+                if (state == LS_TRAV || state == LS_HELP) {
+                    trav_iter<STACK, CNT, FEAT>(p, ray, tr, L, cnt);
+                    if (tr.nodeAddr == kSentinel) {
+                        if (state == LS_HELP) {
+                            state = LS_HELPDONE;           // its best hit waits for the owner (help_step)
+                        } else if (pend == 0) {
+                            trav_finish(tr, hr);
+                            state = LS_SHADE;
+                        }                                  // else: the owner waits for its helpers
+                    }
+                }
+            }
+        }
+        bool ended = false;
+        if (state == LS_SHADE) {
+            vr4 out;
+            if (bounce_step<CNT, FEAT>(p, ray, hr, ps, out, cnt)) {
+                store_path(p, q, slot, out, ps.depth);
+                if constexpr ((FEAT & F_SMALL) != 0u) {
+                    if (p.path_cost)
+                        p.path_cost[(size_t)q * p.path_stride + slot] = (uint8_t)(cnt.work < 510u ? cnt.work >> 1 : 255u);
+                }
+                ended = true;
+            } else {
+                state = LS_SETUP;
+            }
+        }
+        const unsigned long long em = __ballot(ended);
+        if (em != 0ull) {
+            const uint32_t need = (uint32_t)__popcll(em);
+            uint32_t nsub = cur_sub, nq = cur_q;
+            if (next + need > 64u && cur_sub != ~0u) grab(nsub, nq);
+            if (ended) {
+                const uint32_t r = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                if (r < 64u) start(cur_sub, cur_q, r);
+                else start(nsub, nq, r - 64u);
+            }
+            if (next + need > 64u) { cur_sub = nsub; cur_q = nq; next = next + need - 64u; }
+            else next += need;
+        }
+        if (__ballot(state != LS_DONE) == 0ull) break;
+    }
+    if (CNT) flush_counts(p, cnt, lane, true);
+}
+
+// ---- host launchers --------------------------------------------------------
+// Feature specialisations, smallest first (BASELINE configs C1..C5); the
+// generic kernel covers everything else, deep trees and the counting variant.
+constexpr uint32_t kFeatAll =
+    F_CORNELL | F_EXAMPLE | F_VIEW_BRDF | F_MESH | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC | F_STRICT;
+static_assert((kFeatAll & F_COUNT_EXEC) == 0u, "F_COUNT_EXEC is a compile-time kernel variant, not a scene flag");
+constexpr uint32_t kFeatCornellMesh = F_CORNELL | F_MESH;                                  // C2
+constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                              // C1
+constexpr uint32_t kFeatHdriMesh = F_MESH;                                                 // C5
+constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;        // C3
+constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
+
+// Multi-frame launches of fewer than 2^24 paths (shards) on the small-launch
+// kernels (F_SMALL: helper lanes, per-path costs, longest-first order) or,
+// with 0, on the whole-frame kernels in 256-thread blocks
+#ifndef VR_SHARD_SMALL
+#define VR_SHARD_SMALL 0
+#endif
+template <int STACK, uint32_t FEAT>
+inline void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
+{
+    // one-frame launches trace the camera ray in the path kernel (a separate
+    // instantiation); the instrumented copy always takes the primary pass
+    if constexpr ((FEAT & (F_INLINE_PRIM | F_COUNT_EXEC)) == 0u) {
+        if (p.inline_prim) { launch_wave<STACK, FEAT | F_INLINE_PRIM>(p, n_tiles, s); return; }
+    }
+    if constexpr ((FEAT & (F_SMALL | F_COUNT_EXEC)) == 0u) {
+        if (p.small_blocks && (VR_SHARD_SMALL != 0 || (FEAT & F_INLINE_PRIM) != 0u)) {
+            launch_wave<STACK, FEAT | F_SMALL>(p, n_tiles, s);
+            return;
+        }
+    }
+    if constexpr ((FEAT & F_INLINE_PRIM) == 0u)
+        hipLaunchKernelGGL((primary_kernel<STACK, FEAT & ~F_SMALL>), dim3(n_tiles), dim3(kBlockThreads), 0, s, p);
+    // one resident set: path_waves(STACK, C) waves per SIMD, 4 SIMDs per CU;
+    // small launches (and the instrumented copy of one) in the smaller blocks
+    constexpr bool C = cornell_kernel<FEAT>();
+    constexpr int BT = ((FEAT & F_SMALL) != 0u) ? wave_block_small(STACK, C) : wave_block(STACK, C);
+    constexpr int BTS = wave_block_small(STACK, C);
+    // counted, or multi-frame shards on the whole-frame kernel: block size picked at run time below
+    constexpr bool runtime_bt = (FEAT & F_COUNT_EXEC) != 0u || ((FEAT & F_SMALL) == 0u && VR_SHARD_SMALL == 0);
+    constexpr int B = (runtime_bt && BTS != BT) ? 0 : BT;
+    // blocks per CU: the kernel's full residency, or fewer under a waves-per-SIMD cap
+    auto per_cu = [&](int bt) {
+        const uint32_t full = (uint32_t)path_blocks_per_cu(STACK, bt, C);
+        if (p.waves_cap == 0u) return full;
+        const uint32_t capped = p.waves_cap * 4u * 64u / (uint32_t)bt;
+        return capped < 1u ? 1u : (capped < full ? capped : full);
+    };
+    if constexpr (B == 0) {
+        if (p.small_blocks) {
+            hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * per_cu(BTS)), dim3(BTS), 0, s, p);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BT>), dim3(p.wave_blocks * per_cu(BT)), dim3(BT), 0, s, p);
+}
+
+// One scene specialisation, production (FEAT) or instrumented
+// (FEAT | F_COUNT_EXEC: same launch shape, residency, node-loop threshold and
+// queues as the production kernel of the same scene, plus load counters).
+template <uint32_t FEAT>
+inline void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
+{
+    constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;
+    if constexpr ((FEAT & F_MESH) == 0u) {
+        // sphere-only scenes: one pixel per thread, primary hit shared by its paths
+        hipLaunchKernelGGL((render_kernel<16, CNT, FEAT>), dim3(n_tiles * p.split), dim3(kBlockThreads), 0, s, p);
+    } else {
+        // mesh scenes: the path-pool kernel (traversal divergence)
+        if ((p.flags & F_MESH) == 0u)
+            hipLaunchKernelGGL((render_kernel<16, CNT, FEAT>), dim3(n_tiles * p.split), dim3(kBlockThreads), 0, s, p);
+        else if (stack_depth <= 16)
+            launch_wave<16, FEAT>(p, n_tiles, s);
+        else if (stack_depth <= 24)
+            launch_wave<24, FEAT>(p, n_tiles, s);
+        else
+            launch_wave<32, FEAT>(p, n_tiles, s);
+    }
+}
+
+// Per-specialisation launchers, one translation unit each (vr_spec_*.hip);
+// exec = the instrumented copy (F_COUNT_EXEC).
+void launch_spec_c1(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
+void launch_spec_c2(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
+void launch_spec_c3(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
+void launch_spec_c4(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
+void launch_spec_c5(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
+void launch_spec_generic(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
+// trees deeper than 30 levels (64-entry stacks), production or instrumented
+void launch_spec_deep(const RenderParams& p, uint32_t n_tiles, hipStream_t s, bool exec);
+// the reference algorithm's counting variant (strict traversal, in place)
+void launch_counting(const RenderParams& p, uint32_t blocks, int stack_depth, hipStream_t s);
+
+} // namespace vr

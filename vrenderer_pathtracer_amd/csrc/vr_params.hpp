@@ -46,13 +46,10 @@ constexpr int kMaxFramesPerLaunch = 64;
 // [kExecCounterBase, +kExecCounters): node visits served from the LDS copy,
 // triangle loads issued (36 B each), mesh hits shaded, mesh hits shaded
 // through the normal map, and every global lane load issued, by width: 16, 12,
-// 8 and 4 B.  Slots 8..13 hold diagnostic-build phase timers.
+// 8 and 4 B.
 constexpr int kCounters = 8;
 constexpr int kExecCounterBase = 16;
 constexpr int kExecCounters = 8;
-constexpr int kWaveTimesBase = 32;   // -DVR_WAVE_TIMES diagnostic builds: per-wave records from here
-constexpr size_t kPathTimesCap = 4u * 1024u * 1024u;   // -DVR_PATH_TIMES: per-path records after them (paths of a launch)
-constexpr size_t kPathRec = 4;                          // u64 per path record
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
 // render_wave_kernel work queues: RenderParams::n_queues counters (a power of

@@ -1,0 +1,14 @@
+// vr_spec_c1.hip -- the path kernels of scene specialisation C1 (Cornell box + example sphere):
+// production and instrumented (F_COUNT_EXEC) instantiations of vr_kernel.hpp.
+// One translation unit per specialisation, so the build compiles them in parallel.
+#include "vr_kernel.hpp"
+
+namespace vr {
+
+void launch_spec_c1(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec)
+{
+    if (exec) launch_spec<kFeatCornellSphere | F_EXACT | F_COUNT_EXEC>(p, n_tiles, stack_depth, s);
+    else launch_spec<kFeatCornellSphere | F_EXACT>(p, n_tiles, stack_depth, s);
+}
+
+} // namespace vr

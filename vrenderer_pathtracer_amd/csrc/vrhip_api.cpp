@@ -753,15 +753,7 @@ int vrhip_gl_present(vrhip_ctx* c)
     return VRHIP_OK;
 }
 
-#if defined(VR_WAVE_TIMES) && defined(VR_PATH_TIMES)
-constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192 + (int)(vr::kPathRec * vr::kPathTimesCap);   // + kPathRec per path
-#elif defined(VR_WAVE_TIMES) && defined(VR_WAVE_PHASES)
-constexpr int kDebugSlots = vr::kWaveTimesBase + 15 * 8192;  // + per-wave times, then per-wave phase records (8 + 4 u64)
-#elif defined(VR_WAVE_TIMES)
-constexpr int kDebugSlots = vr::kWaveTimesBase + 3 * 8192;   // + per-wave start / end / paths of render_wave_kernel
-#else
-constexpr int kDebugSlots = vr::kWaveTimesBase;
-#endif
+constexpr int kDebugSlots = vr::kExecCounterBase + vr::kExecCounters;
 
 static int ensure_counters(vrhip_ctx* c)
 {
@@ -938,10 +930,6 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kDebugSlots, c->stream));
         p.counters = c->counters;
     }
-#if defined(VR_WAVE_TIMES)
-    if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
-    p.counters = c->counters;   // diagnostic build: per-wave / per-path records
-#endif
     const uint32_t k_max = std::min<uint32_t>(n_frames, (uint32_t)vr::kMaxFramesPerLaunch);
     const uint32_t split_max = count == 1 ? 1u : choose_split(c, n_tiles, k_max);
     p.path_stride = n_tiles * (uint32_t)vr::kBlockThreads;
@@ -1169,33 +1157,6 @@ int vrhip_debug_counters(vrhip_ctx* c, uint64_t out[16], int reset)
     if (reset) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kDebugSlots, c->stream));
     return VRHIP_OK;
 }
-
-#ifdef VR_WAVE_TIMES
-// diagnostic build only (not in vrhip.h): per-wave start, end, paths of the last wave-kernel launch
-extern "C" int vrhip_debug_wave_times(vrhip_ctx* c, uint64_t* out, uint32_t n_waves)
-{
-    if (!c || !out || 3 * (size_t)n_waves > (size_t)(kDebugSlots - vr::kWaveTimesBase)) return fail(VRHIP_ERR_INVALID, "bad argument");
-    int rc = set_device(c); if (rc) return rc;
-    if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(out, c->counters + vr::kWaveTimesBase, sizeof(uint64_t) * 3 * n_waves, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return VRHIP_OK;
-}
-#endif
-#if defined(VR_WAVE_TIMES) && defined(VR_WAVE_PHASES)
-// diagnostic build only: per-wave phase records (8 u64 each, then 4 u64 each of
-// node/leaf rounds and cycles; vr_kernel.hip wave_body); out holds 12 x 8192
-extern "C" int vrhip_debug_wave_phases(vrhip_ctx* c, uint64_t* out, uint32_t n_waves)
-{
-    if (!c || !out || n_waves != 8192) return fail(VRHIP_ERR_INVALID, "bad argument");
-    int rc = set_device(c); if (rc) return rc;
-    if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(out, c->counters + vr::kWaveTimesBase + 3 * 8192, sizeof(uint64_t) * 12 * 8192,
-                           hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return VRHIP_OK;
-}
-#endif
 
 int vrhip_kernel_stats(vrhip_ctx* c, double* total_ms, uint64_t* launches, int reset)
 {
