@@ -315,6 +315,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kms, launches = r.kernel_stats()
+    launch_info = r.last_launch_info()
     t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -430,8 +431,14 @@ def main():
         loads = executed_loads(exec_counts)
         load_bytes = sum(w * n for w, n in loads.items())
         lds_bytes = 32 * exec_counts["node_visits_lds"]        # fp16 node rows from the LDS copy
-        # 12-B path radiances, the 4-B depth term per pixel, the 32-B primary records
-        store_bytes = 12 * own_paths + 4 * owned + (32 * owned if mesh else 0)
+        # stores by launch mode (vrhip_last_launch_info): through the result
+        # scratch, 12-B path radiances + the 4-B depth term per pixel (+ the
+        # 32-B primary records of mesh scenes) and the finish pass's accum /
+        # RGBA8 / depth; in registers (sphere-only launches of one path group)
+        # only the accum / RGBA8 / depth of every pixel
+        store_bytes = 24 * owned
+        if launch_info["use_scratch"]:
+            store_bytes += 12 * own_paths + 4 * owned + (32 * owned if mesh else 0)
         ref_b = reference_bytes(ref_counts, own_paths, owned * F)
         achieved = load_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         roofs = {}
@@ -458,12 +465,17 @@ def main():
             hbm_gbs = traffic / avg_launch_s / 1e9
             roofs["hbm"] = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(hbm_gbs / HBM_PEAK_GBS, 4)}
         ub = unit_busy(CFG)
-        if load_bytes == 0 and ub and "valu" in ub:
-            # VALU issue roof: a wave64 VALU instruction issues over 2 cycles
-            # (MI355X_MICROARCH.md "CU"), so a SIMD retires at most 32 lane-ops
-            # per cycle; busy fraction from the counter passes of this config
-            roofs["valu"] = {"achieved": round(ub["valu"] * VALU_PEAK_TOPS, 2), "peak": VALU_PEAK_TOPS,
-                             "frac": ub["valu"], "unit": "T VALU lane-ops/s"}
+        if load_bytes == 0 and ub and "valu" in ub and "valu_lane_util" in ub:
+            # VALU roof in active lane-ops: a wave64 VALU instruction issues
+            # over 2 cycles (MI355X_MICROARCH.md:54, the guide's figure; not
+            # measured here), so a SIMD retires at most 32 lane-ops per cycle.
+            # achieved = pipe-busy fraction (SQ_INSTS_VALU x 2 cycles) x the
+            # measured VALU lane utilisation, both from this config's counter
+            # pass (profiles/units_<cfg>.json)
+            frac = ub["valu"] * ub["valu_lane_util"]
+            roofs["valu"] = {"achieved": round(frac * VALU_PEAK_TOPS, 2), "peak": VALU_PEAK_TOPS,
+                             "frac": round(frac, 4), "pipe_busy": ub["valu"], "lane_util": ub["valu_lane_util"],
+                             "unit": "T VALU lane-ops/s"}
         if load_bytes == 0:
             # sphere-only scenes without textures (C1): no global loads on the
             # path -- the sphere tests and libm are VALU work, priced by the
@@ -479,6 +491,8 @@ def main():
                     "executed_load_bytes_per_launch": int(load_bytes),
                     "lane_loads_per_launch": {f"b{8 * w}": int(n) for w, n in loads.items()},
                     "lds_node_bytes_per_launch": int(lds_bytes), "store_bytes_per_launch": int(store_bytes),
+                    "launch": launch_info,
+                    "shared_miss_paths_per_launch": int(exec_counts.get("shared_miss_paths", 0)),
                     "roofs": roofs,
                     "gather_position": gpos,
                     "traffic_source": traffic_src,
@@ -516,6 +530,10 @@ def main():
             "mrays_per_s": round(mrays, 3),
             "rays_per_path": round(rays_per_path, 4),
             "mrays_per_s_traced": round(value * rays_per_path_traced, 3),
+            # paths whose result was their pixel's shared escape radiance
+            # (sphere-only HDRI scenes: the camera ray escapes, no jitter), so
+            # they made no HDRI fetch of their own (render_kernel)
+            "shared_escape_path_frac": round(exec_counts.get("shared_miss_paths", 0) / max(owned * 2 * F, 1), 4),
             "rays_per_path_traced": round(rays_per_path_traced, 4),
             "mrays_note": ("mrays_per_s is reference-equivalent: intersectScene calls of the reference algorithm "
                            "(two camera rays per pixel per frame, SURVEY 8d) at this path rate; "

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define VRHIP_ABI_VERSION 1
+#define VRHIP_ABI_VERSION 2
 
 typedef enum vrhip_status {
     VRHIP_OK = 0,
@@ -178,9 +178,12 @@ int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *time
  * (36 B each; an odd leaf's last pair loads its triangle twice), [10] mesh
  * hits shaded, [11] of those through the normal map, [12..15] every global
  * lane load the production kernels issue, by width: 16 B, 12 B, 8 B, 4 B
- * (nodes, triangles, primary records, attributes, texels, BRDF entries).
+ * (nodes, triangles, primary records, attributes, texels, BRDF entries),
+ * [16] paths that took their pixel's shared escape radiance (sphere-only HDRI
+ * scenes: a camera ray that escapes gives every path of the pixel the same
+ * result, fetched once per pixel and launch).
  * Synchronous. */
-#define VRHIP_PROFILE_COUNTERS 16
+#define VRHIP_PROFILE_COUNTERS 17
 int vrhip_render_profiled(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
                           uint64_t counters[VRHIP_PROFILE_COUNTERS]);
 int vrhip_sync(vrhip_ctx *ctx);
@@ -272,6 +275,12 @@ int vrhip_last_kernel_ms(vrhip_ctx *ctx, float *ms);
  * span includes time shared with the neighbouring launch.  Waits for the
  * pending launches. */
 int vrhip_kernel_stats(vrhip_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
+/* Shape of the last production launch of vrhip_render (measurement; no
+ * reference counterpart): path groups per pixel (sphere-only scenes), whether
+ * the paths' results went through the result scratch and the finish pass (1)
+ * or were accumulated in registers in path order (0), and the kernel family
+ * (0 render_kernel, 1 path-pool kernel, 2 render service). */
+int vrhip_last_launch_info(vrhip_ctx *ctx, uint32_t *split, uint32_t *use_scratch, uint32_t *kind);
 /* Vector-memory gather roof of `device` (the ceiling the path kernel's
  * node, triangle and attribute fetches run against; no reference
  * counterpart): raw buffer loads of width_bytes (4, 8, 12 or 16) per lane

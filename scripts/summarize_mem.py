@@ -50,9 +50,11 @@ def main():
     src, name, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
     paths = int(sys.argv[4]) if len(sys.argv) > 4 else None
     per = defaultdict(list)
+    kernels = set()
     for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             if production_wave(r["Kernel_Name"]):
+                kernels.add(r["Kernel_Name"].split("(")[0])
                 per[r["Counter_Name"]].append((int(r["Start_Timestamp"]), float(r["Counter_Value"]),
                                                int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     m, dur = {}, {}
@@ -63,7 +65,8 @@ def main():
         dur[k] = sum(d for _, _, d in t) / len(t)
     lines = [f"# Issue and memory-pipeline counters, {name} ({cfg})", "",
              f"Source: `scripts/gpu_mem.sh` (one counter group per rocprofv3 pass) on `bench.py --config {cfg}`; "
-             f"means over the {TIMED} timed dispatches of the production `render_wave_kernel`.", "",
+             f"means over the {TIMED} timed dispatches of the production kernel "
+             + ", ".join(f"`{k}`" for k in sorted(kernels)) + ".", "",
              "| counter | per dispatch |", "|---|---|"]
     lines += [f"| {k} | {v:.4g} |" for k, v in sorted(m.items())]
     g = m.get("GRBM_GUI_ACTIVE")
@@ -112,6 +115,9 @@ def main():
                 units[key] = round(m[k] / (CUS * cyc), 4)
         if "SQ_INSTS_VALU" in m:
             units["valu"] = round(m["SQ_INSTS_VALU"] * 2 / (4 * CUS * cyc), 4)
+        if "SQ_THREAD_CYCLES_VALU" in m and m.get("SQ_ACTIVE_INST_VALU"):
+            units["valu_lane_util"] = round(m["SQ_THREAD_CYCLES_VALU"] / (64 * m["SQ_ACTIVE_INST_VALU"]), 4)
+        units["kernels"] = sorted(kernels)
         json.dump(units, open(os.path.join(REPO, "profiles", f"units_{cfg.lower()}.json"), "w"), indent=1)
     print("\n".join(lines))
 

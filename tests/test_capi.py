@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(native):
     declared = set(_native.header_symbols())
     assert declared, "no symbols parsed from include/vrhip.h"
     assert declared <= exported, sorted(declared - exported)
-    assert native.vrhip_abi_version() == 1
+    assert native.vrhip_abi_version() == 2
 
 
 def _has_gpu(native):
@@ -138,6 +138,29 @@ def test_validate_flat_rejects_corruption(native):
     bad = {k: v.copy() for k, v in flat.items()}
     term = np.where(bad["verts"][:, 0].view(np.uint32) == 0x80000000)[0]
     bad["verts"][term[-1], 0] = 1.0                                              # lost terminator
+    with pytest.raises(_native.VRHIPError):
+        validate_flat(bad)
+
+
+def test_validate_flat_rejects_shared_nodes_and_leaves(native):
+    """The device layout keys the equal-t tie-break on each triangle's unique
+    root path (vrhip_api.cpp tri_paths), so the flattened BVH must be a tree
+    (the reference's LIFO flatten always is, src/vRendererCuda.cpp:204-279):
+    an inner node or a leaf run reached from two parents is rejected before
+    upload (vrhip_upload_mesh_flat validates first)."""
+    flat = build_flat(scenes.torus_knot(20, 10))
+    kids = flat["bvh"][3::4, :2].view(np.int32)            # child indices of every node
+    inner = [(n, c, int(kids[n, c])) for n in range(kids.shape[0]) for c in range(2) if kids[n, c] > 0]
+    leaves = [(n, c, int(kids[n, c])) for n in range(kids.shape[0]) for c in range(2) if kids[n, c] < 0]
+    assert len(inner) >= 2 and len(leaves) >= 2
+    bad = {k: v.copy() for k, v in flat.items()}
+    (n0, c0, i0), (n1, c1, _) = inner[0], inner[-1]
+    bad["bvh"][4 * n1 + 3, c1] = np.array([i0], np.int32).view(np.float32)[0]   # a second parent of node i0
+    with pytest.raises(_native.VRHIPError):
+        validate_flat(bad)
+    bad = {k: v.copy() for k, v in flat.items()}
+    (n0, c0, l0), (n1, c1, _) = leaves[0], leaves[-1]
+    bad["bvh"][4 * n1 + 3, c1] = np.array([l0], np.int32).view(np.float32)[0]   # one leaf run, two parents
     with pytest.raises(_native.VRHIPError):
         validate_flat(bad)
 

@@ -16,6 +16,7 @@ import pytest
 
 import pyoracle as po
 from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math, selftest_rcp, selftest_sqrt
+from vrenderer_pathtracer_amd._native import VRHIPError
 
 pytestmark = pytest.mark.gpu
 
@@ -147,8 +148,8 @@ def test_render_bitexact_vs_portable_oracle(native, oracle, cfg, w, h, frames):
 def test_render_tolerance_vs_glibc_oracle(native, oracle, cfg, w, h, frames):
     """Default (t-culled) GPU render vs the oracle with glibc's libm -- the
     semantics of the survey's probe of the reference -- at equal spp: image
-    RMSE of accum/frames below the north-star 1e-3 and >= 99 % of pixels with
-    max-channel |delta| <= 1e-3."""
+    RMSE of accum/frames below the north-star 1e-3 and >= 99.5 % of pixels
+    with max-channel |delta| <= 1e-3 (TOL_RMSE, TOL_PIX_FRAC)."""
     sc = scenes.make_scene(cfg, w, h)
     times = [sc["time"] + 11 * i for i in range(frames)]
     ga, _, _, _ = gpu_render(sc, frames, times)
@@ -159,6 +160,38 @@ def test_render_tolerance_vs_glibc_oracle(native, oracle, cfg, w, h, frames):
     rmse = float(np.sqrt(((g - o) ** 2).mean()))
     frac = float((d <= 1e-3).mean())
     print(f"{cfg} {w}x{h} {frames} frames vs glibc oracle: RMSE {rmse:.3e}, {frac:.5f} of pixels within 1e-3")
+    assert rmse < TOL_RMSE, rmse
+    assert frac >= TOL_PIX_FRAC, frac
+
+
+@pytest.mark.parametrize("cfg,frames,rows", [
+    ("C2", 8, None),             # 1280x720 x 8 frames: 14.7 M paths
+    ("C3", 8, None),             # 1280x720 x 8 frames
+    ("C4", 4, None),             # 1920x1080 (rendered 1920x1072) x 4 frames
+    ("C5", 8, (1056, 1104)),     # 3840x2160, a 48-row band through the knot's middle (oracle row range)
+])
+def test_render_tolerance_vs_glibc_oracle_baseline_size(native, oracle, cfg, frames, rows):
+    """The north-star tolerance at the BASELINE.json resolutions: the default
+    (t-culled) GPU render of the whole frame against the oracle with glibc's
+    libm (the semantics of the survey's probe of the reference), per-pixel
+    radiance accum/frames over the rendered rows (for C5 a band of rows,
+    oracle/vro.c row range: the whole 4K frame would take minutes of CPU):
+    image RMSE < TOL_RMSE and >= TOL_PIX_FRAC of pixels within 1e-3."""
+    sc = scenes.make_scene(cfg)
+    times = [sc["time"] + 13 * i for i in range(frames)]
+    ga, _, _, nf = gpu_render(sc, frames, times)
+    assert nf == frames
+    H = (sc["height"] // 16) * 16
+    r0, r1 = rows if rows else (0, H)
+    oa, _, _, _ = po.render(sc, frames=frames, times=times, libm=po.LIBM_GLIBC, rows=(r0, r1))
+    g = rendered(ga, sc)[r0:r1, ..., :3] / frames
+    o = rendered(oa, sc)[r0:r1, ..., :3] / frames
+    assert np.any(o != 0)
+    d = np.abs(g - o).max(-1)
+    rmse = float(np.sqrt(((g - o) ** 2).mean()))
+    frac = float((d <= 1e-3).mean())
+    print(f"{cfg} {sc['width']}x{sc['height']} rows {r0}-{r1} {frames} frames vs glibc oracle: RMSE {rmse:.3e}, "
+          f"{frac:.6f} of {d.size} pixels within 1e-3")
     assert rmse < TOL_RMSE, rmse
     assert frac >= TOL_PIX_FRAC, frac
 
@@ -203,7 +236,9 @@ def test_profiled_render_is_the_production_render(native, cfg, w, h, frames):
     assert e["node_visits_lds"] <= e["node_visits"] <= ref["node_visits"]
     assert e["tri_tests"] <= ref["tri_tests"] and e["tri_loads"] >= e["tri_tests"]
     assert e["nmap_hits"] <= e["mesh_hits"]
-    assert e["hdr_fetches"] == ref["hdr_fetches"] and e["brdf_fetches"] <= ref["brdf_fetches"]
+    # escaped camera rays of sphere-only HDRI scenes are fetched once per pixel (shared_miss_paths)
+    assert e["hdr_fetches"] <= ref["hdr_fetches"] and e["brdf_fetches"] <= ref["brdf_fetches"]
+    assert e["hdr_fetches"] + e["shared_miss_paths"] >= ref["hdr_fetches"]
     if sc.get("mesh_flat") is None:
         assert e["node_visits"] == 0 and e["mesh_hits"] == 0
     else:
@@ -233,12 +268,18 @@ def test_comm_gather_single_rank_through_c_abi(native):
     r = VRendererHIP(0)
     scenes.load_into(r, sc)
     r.comm_init(0, 1, comm_unique_id())
+    # the gather buffers are sized for the communicator's tiling: changing
+    # it while the communicator exists is refused (vrhip_set_tiling)
+    with pytest.raises(VRHIPError):
+        r.set_tiling(0, 2)
     r.render(frames=2, times=times, sync=False)
     r.comm_gather(WHAT_RGBA8)
     r.comm_gather(WHAT_ACCUM)
     r.sync()
     acc, rgba = r.read_accum(), r.read_rgba8()
     r.comm_destroy()
+    r.set_tiling(0, 2)              # free again once the communicator is gone
+    r.set_tiling(0, 1)
     r.cleanUp()
     assert_bitexact(acc, base[0], sc, "accum")
     assert_bitexact(rgba, base[1], sc, "rgba8")
@@ -409,7 +450,11 @@ def _random_soup(seed, n, leaf):
 def test_random_soup_bitexact_vs_portable_oracle(native, oracle, cfg, leaf):
     """Overlapping random triangles (odd leaf sizes exercise the paired
     triangle loads' tail): strict traversal bit-exact against the oracle, the
-    default t-culled traversal equal to strict up to fp32 corner cases."""
+    default t-culled traversal equal to strict (DESIGN.md "Equal-t ties": the
+    tie-break makes the hit independent of the visit order; what could still
+    differ is a triangle whose hit distance exceeds the slab entry of its box
+    by more than the 2^-10 culling margin through fp32 rounding -- none
+    measured)."""
     sc = scenes.make_scene(cfg, 96, 64)
     sc["mesh_flat"] = _random_soup(11 + leaf, 1500, leaf)
     times = [sc["time"], sc["time"] + 1]
@@ -419,7 +464,7 @@ def test_random_soup_bitexact_vs_portable_oracle(native, oracle, cfg, leaf):
     assert_bitexact(srgba, orgba, sc, "rgba8 (strict)")
     ca, _, _, _ = gpu_render(sc, 2, times)
     diff = (rendered(ca, sc).view(np.uint32) != rendered(sa, sc).view(np.uint32)).any(-1)
-    assert diff.mean() <= 1e-3, int(diff.sum())
+    assert int(diff.sum()) == 0, int(diff.sum())
 
 
 @pytest.mark.parametrize("cfg", ["C2", "C3"])
@@ -439,7 +484,7 @@ def test_stack24_tree_bitexact_vs_portable_oracle(native, oracle, cfg):
     assert_bitexact(srgba, orgba, sc, "rgba8 (strict)")
     ca, _, _, _ = gpu_render(sc, 2, times)
     diff = (rendered(ca, sc).view(np.uint32) != rendered(sa, sc).view(np.uint32)).any(-1)
-    assert diff.mean() <= 1e-3, int(diff.sum())
+    assert int(diff.sum()) == 0, int(diff.sum())
 
 
 @pytest.mark.parametrize("cfg", ["C2", "C3"])
@@ -547,26 +592,31 @@ def test_strict_traversal_bitexact_vs_portable_oracle(native, oracle, cfg, w, h)
 @pytest.mark.parametrize("cfg,frames", [("C2", 2), ("C3", 2), ("C5", 1)])
 def test_culled_vs_strict_full_frame(native, cfg, frames):
     """t-culled traversal against the reference's visit-every-pierced-box
-    traversal at full BASELINE resolution: the closest hit may differ only in
-    fp32 corner cases; bound the fraction of affected pixels."""
+    traversal at full BASELINE resolution: identical (DESIGN.md "Equal-t
+    ties" and the 2^-10 culling margin; 0 pixels measured since round 2)."""
     sc = scenes.make_scene(cfg)
     a_cull, _, _, _ = gpu_render(sc, frames)
     a_strict, _, _, _ = gpu_render(sc, frames, strict=True)
     diff = (rendered(a_cull, sc).view(np.uint32) != rendered(a_strict, sc).view(np.uint32)).any(-1)
     n = int(diff.sum())
     print(f"{cfg}: {n} of {diff.size} pixels differ between culled and strict traversal")
-    assert n / diff.size <= 1e-5
+    assert n == 0
 
 
-@pytest.mark.parametrize("cfg,tiling,overlap", [("C3", None, 0), ("C2", (1, 3), -1), ("C5", (0, 2), 1)])
-def test_longest_first_order_is_scheduling_only(native, oracle, cfg, tiling, overlap):
+@pytest.mark.parametrize("cfg,tiling,overlap,size", [("C3", None, 0, (160, 112)), ("C2", (1, 3), -1, (160, 112)),
+                                                     ("C5", (0, 2), 1, (96, 64)),
+                                                     ("C2", None, 0, (320, 224)), ("C2", None, 1, (320, 224))])
+def test_longest_first_order_is_scheduling_only(native, oracle, cfg, tiling, overlap, size):
     """Small launches (one frame per call, shards) take their sub-tiles in the
     order the previous launch on the same scratch measured (per-path costs
     summed per sub-tile by the finish pass, sorted per XCD by order_kernel).
     Consecutive one-frame calls -- the second and later ones ordered, on one
     path stream or on three -- equal the band-order render bit for bit, and
-    the oracle."""
-    sc = scenes.make_scene(cfg, 160, 112) if cfg != "C5" else scenes.make_scene("C5", 96, 64, knot=(150, 75))
+    the oracle.  320x224 has 1,120 sub-tiles, more than 8 XCDs x
+    VR_XCD_BANDS = 1,024: the order lists' second band (g >= 1 in grab's
+    lookup, every 720p and 4K one-frame launch) is exercised too."""
+    w, h = size
+    sc = scenes.make_scene(cfg, w, h) if cfg != "C5" else scenes.make_scene("C5", w, h, knot=(150, 75))
     times = [sc["time"] + 7 * i for i in range(7)]
     outs = []
     for order in ("1", "0"):

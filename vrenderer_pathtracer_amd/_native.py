@@ -86,6 +86,7 @@ _SIGNATURES = {
     "vrhip_comm_gather": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "vrhip_comm_destroy": (ctypes.c_int, [_ctx]),
     "vrhip_last_kernel_ms": (ctypes.c_int, [_ctx, _f]),
+    "vrhip_last_launch_info": (ctypes.c_int, [_ctx, _u32, _u32, _u32]),
     "vrhip_bvh_info": (ctypes.c_int, [_ctx, _u32, _u32, _u32]),
     "vrhip_selftest_math": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _f, _f, _f, ctypes.c_size_t]),
     "vrhip_selftest_rcp": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,

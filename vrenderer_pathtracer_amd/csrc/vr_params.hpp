@@ -46,10 +46,11 @@ constexpr int kMaxFramesPerLaunch = 64;
 // [kExecCounterBase, +kExecCounters): node visits served from the LDS copy,
 // triangle loads issued (36 B each), mesh hits shaded, mesh hits shaded
 // through the normal map, and every global lane load issued, by width: 16, 12,
-// 8 and 4 B.
+// 8 and 4 B, and paths whose result was the shared escape radiance of
+// their pixel's camera ray (render_kernel; no HDRI fetch of their own).
 constexpr int kCounters = 8;
 constexpr int kExecCounterBase = 16;
-constexpr int kExecCounters = 8;
+constexpr int kExecCounters = 9;
 constexpr int kBand = 16;            // block height of the reference launch (PathTracer.cu:887)
 constexpr int kBlockThreads = 256;   // 16x16 tile, four 8x8 wave64 sub-tiles
 // render_wave_kernel work queues: RenderParams::n_queues counters (a power of

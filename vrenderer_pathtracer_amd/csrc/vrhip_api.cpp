@@ -16,6 +16,7 @@
 #include <cstring>
 #include <deque>
 #include <fstream>
+#include <algorithm>
 #include <array>
 #include <queue>
 #include <string>
@@ -132,7 +133,12 @@ struct vrhip_ctx {
     bool timed = false;          // ev0/ev1 hold the last render
     double kernel_ms_total = 0.0;    // union of the launches' render-kernel spans (overlapping launches count once)
     uint64_t launches_total = 0;
-    hipEvent_t kev_last_end = nullptr;   // end event of the latest-ending span accounted so far
+    uint32_t last_split = 1, last_use_scratch = 0, last_kind = 0;   // vrhip_last_launch_info
+    // spans as [start, end) in ms after kev_origin (the start event of the
+    // first span since the last reset), merged into disjoint intervals: launches
+    // on different path streams can start out of queue order
+    hipEvent_t kev_origin = nullptr;
+    std::vector<std::pair<double, double>> kev_union;
     unsigned long long* counters = nullptr;
     // GL interop (colour, depth textures registered by the display host)
     hipGraphicsResource_t gl_res[2] = { nullptr, nullptr };
@@ -357,45 +363,44 @@ void build_nodes16(DeviceMesh& dm)
 bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const vr4* normals,
                       const vr4* tangents, const vr2* uvs, DeviceMesh& dm, std::string& why)
 {
+    // The input must be a tree (vr::validate_flat, which every upload runs
+    // first, rejects a node or leaf run with two parents): each triangle then
+    // has ONE root path, the key of the equal-t tie-break (tri_paths).  A
+    // shared node or leaf is refused here too rather than merged, since a
+    // merged copy would give its triangles the path of one parent only.
     dm.nodes.assign((const vr4*)bvh, (const vr4*)bvh + n_bvh_f4);
-    std::unordered_map<int32_t, int32_t> leaf_code;
     std::vector<size_t> st{ 0 };
     std::vector<uint8_t> seen(n_bvh_f4 / 4, 0);
+    std::unordered_map<int32_t, int> leaf_seen;
     while (!st.empty()) {
         const size_t off = st.back();
         st.pop_back();
-        if (seen[off / 4]) continue;
+        if (seen[off / 4]) { why = "flattened BVH is not a tree (a node has two parents)"; return false; }
         seen[off / 4] = 1;
         float* idxf = &dm.nodes[off + 3].x;
         for (int ch = 0; ch < 2; ++ch) {
             int32_t idx;
             std::memcpy(&idx, &idxf[ch], 4);
             if (idx >= 0) { st.push_back((size_t)idx); continue; }
-            auto it = leaf_code.find(idx);
-            int32_t code;
-            if (it != leaf_code.end()) {
-                code = it->second;
-            } else {
-                const size_t first = dm.tris.size() / 3;
-                size_t s = (size_t)(~idx), count = 0;
-                for (;;) {
-                    uint32_t b;
-                    std::memcpy(&b, &verts[s].x, 4);
-                    if (b == 0x80000000u) break;
-                    for (int k = 0; k < 3; ++k) {
-                        dm.tris.push_back(vr3{ verts[s + k].x, verts[s + k].y, verts[s + k].z });
-                        dm.normals.push_back(normals[s + k]);
-                        dm.tangents.push_back(tangents[s + k]);
-                        dm.uvs.push_back(uvs[s + k]);
-                    }
-                    s += 3;
-                    ++count;
+            if (!leaf_seen.emplace(idx, 1).second) { why = "flattened BVH is not a tree (a leaf has two parents)"; return false; }
+            const size_t first = dm.tris.size() / 3;
+            size_t s = (size_t)(~idx), count = 0;
+            for (;;) {
+                uint32_t b;
+                std::memcpy(&b, &verts[s].x, 4);
+                if (b == 0x80000000u) break;
+                for (int k = 0; k < 3; ++k) {
+                    dm.tris.push_back(vr3{ verts[s + k].x, verts[s + k].y, verts[s + k].z });
+                    dm.normals.push_back(normals[s + k]);
+                    dm.tangents.push_back(tangents[s + k]);
+                    dm.uvs.push_back(uvs[s + k]);
                 }
-                if (count >= (1u << kLeafCountBits)) { why = "leaf with >= 128 triangles"; return false; }
-                if (first >= (1u << (31 - kLeafCountBits))) { why = "more than 16M triangle references"; return false; }
-                code = ~(int32_t)((first << kLeafCountBits) | count);
-                leaf_code.emplace(idx, code);
+                s += 3;
+                ++count;
             }
+            if (count >= (1u << kLeafCountBits)) { why = "leaf with >= 128 triangles"; return false; }
+            if (first >= (1u << (31 - kLeafCountBits))) { why = "more than 16M triangle references"; return false; }
+            const int32_t code = ~(int32_t)((first << kLeafCountBits) | count);
             std::memcpy(&idxf[ch], &code, 4);
         }
     }
@@ -544,7 +549,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (auto& pr : c->kev_pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (hipEvent_t e : c->kev_free) (void)hipEventDestroy(e);
-    if (c->kev_last_end) (void)hipEventDestroy(c->kev_last_end);
+    if (c->kev_origin) (void)hipEventDestroy(c->kev_origin);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return VRHIP_OK;
@@ -767,9 +772,10 @@ static int ensure_counters(vrhip_ctx* c)
 // Adds the render-kernel times of completed launches to the totals; with
 // `wait`, waits for all of them.  Never blocks otherwise, so a render call
 // does not wait for the previous one (launches pipeline, see render_impl).
-// Launches on the path streams can overlap: the total is the union of the
-// spans (each span counted from the later of its start and the latest end
-// accounted before it), so it never exceeds the wall time they cover.
+// Launches on the path streams can overlap and need not start in queue
+// order: every span is placed on one time line (ms after kev_origin) and
+// the total is the length of the union of the spans, so it never exceeds the
+// wall time they cover and is never less than the longest span.
 static int account_pending(vrhip_ctx* c, bool wait)
 {
     while (!c->kev_pending.empty()) {
@@ -781,27 +787,33 @@ static int account_pending(vrhip_ctx* c, bool wait)
             if (q == hipErrorNotReady) break;
             if (q != hipSuccess) return fail(VRHIP_ERR_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
         }
-        float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
-        bool newest_end = true;
-        if (c->kev_last_end) {
-            float gap = 0.f, ext = 0.f;          // start and end relative to the latest end so far
-            HIP_TRY(hipEventElapsedTime(&gap, c->kev_last_end, pr.first));
-            HIP_TRY(hipEventElapsedTime(&ext, c->kev_last_end, pr.second));
-            if (gap < 0.f) ms = ext > 0.f ? ext : 0.f;     // starts inside the covered time
-            newest_end = ext > 0.f;
+        bool keep_start = false;
+        if (!c->kev_origin) { c->kev_origin = pr.first; keep_start = true; }
+        float t0 = 0.f, t1 = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t0, c->kev_origin, pr.first));
+        HIP_TRY(hipEventElapsedTime(&t1, c->kev_origin, pr.second));
+        if (t1 > t0) {
+            // insert [t0, t1) and merge the intervals it touches
+            auto& u = c->kev_union;
+            double lo = t0, hi = t1;
+            std::vector<std::pair<double, double>> out;
+            out.reserve(u.size() + 1);
+            for (const auto& iv : u) {
+                if (iv.second < lo || iv.first > hi) out.push_back(iv);
+                else { lo = std::min(lo, iv.first); hi = std::max(hi, iv.second); }
+            }
+            out.emplace_back(lo, hi);
+            std::sort(out.begin(), out.end());
+            u.swap(out);
         }
-        c->kernel_ms_total += ms;
         c->launches_total += 1;
         c->kev_pending.pop_front();
-        c->kev_free.push_back(pr.first);
-        if (newest_end) {
-            if (c->kev_last_end) c->kev_free.push_back(c->kev_last_end);
-            c->kev_last_end = pr.second;
-        } else {
-            c->kev_free.push_back(pr.second);
-        }
+        if (!keep_start) c->kev_free.push_back(pr.first);
+        c->kev_free.push_back(pr.second);
     }
+    double tot = 0.0;
+    for (const auto& iv : c->kev_union) tot += iv.second - iv.first;
+    c->kernel_ms_total = tot;
     return VRHIP_OK;
 }
 
@@ -1010,8 +1022,10 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             // scratch at once -- a lane first used behind a launch in flight
             // would otherwise allocate there (hipMalloc waits for the device)
             // and serialise the overlapped launches; whole frames run on lane 0
+            // (only where overlap can happen: never with vrhip_set_overlap(0))
+            const bool all_lanes = ovl_size && c->overlap != 0 && count == 0;
             for (auto& ln : c->lane)
-                if ((ovl_size || &ln == &l) && (rc = ensure_lane(c, ln, need, p.path_stride)) != VRHIP_OK) return rc;
+                if ((all_lanes || &ln == &l) && (rc = ensure_lane(c, ln, need, p.path_stride)) != VRHIP_OK) return rc;
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = reinterpret_cast<vr::vr3*>(l.paths); p.path_w = reinterpret_cast<float*>(p.paths + need);
             p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
@@ -1037,6 +1051,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             c->kev_pending.emplace_back(k0, k1);
             HIP_TRY(hipEventRecord(k0, rs));
         }
+        if (count == 0) { c->last_split = p.split; c->last_use_scratch = p.use_scratch; c->last_kind = wave_kernel ? 1u : 0u; }
         int e = vr::launch_render(p, n_tiles, stack, count, rs);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
         if (n_tiles) HIP_TRY(hipEventRecord(k1, rs));
@@ -1168,8 +1183,18 @@ int vrhip_kernel_stats(vrhip_ctx* c, double* total_ms, uint64_t* launches, int r
     if (reset) {
         c->kernel_ms_total = 0.0;
         c->launches_total = 0;
-        if (c->kev_last_end) { c->kev_free.push_back(c->kev_last_end); c->kev_last_end = nullptr; }
+        c->kev_union.clear();
+        if (c->kev_origin) { c->kev_free.push_back(c->kev_origin); c->kev_origin = nullptr; }
     }
+    return VRHIP_OK;
+}
+
+int vrhip_last_launch_info(vrhip_ctx* c, uint32_t* split, uint32_t* use_scratch, uint32_t* kind)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    if (split) *split = c->last_split;
+    if (use_scratch) *use_scratch = c->last_use_scratch;
+    if (kind) *kind = c->last_kind;
     return VRHIP_OK;
 }
 

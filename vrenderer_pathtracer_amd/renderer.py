@@ -389,12 +389,12 @@ class VRendererHIP:
             arr = (ctypes.c_uint32 * frames)(*[int(t) & 0xFFFFFFFF for t in times])
         if time_seed is None:
             time_seed = self.default_time if self.default_time is not None else int(_time.time() * 1000)
-        c = (ctypes.c_uint64 * 16)()
+        c = (ctypes.c_uint64 * 17)()
         check(self._lib.vrhip_render_profiled(self._need_ctx(), frames, arr, int(time_seed) & 0xFFFFFFFF, c),
               "vrhip_render_profiled")
         names = ["rays", "node_visits", "slot_reads", "tri_tests", "attr_bytes", "tex_fetches", "hdr_fetches",
                  "brdf_fetches", "node_visits_lds", "tri_loads", "mesh_hits", "nmap_hits", "lane_loads_b128",
-                 "lane_loads_b96", "lane_loads_b64", "lane_loads_b32"]
+                 "lane_loads_b96", "lane_loads_b64", "lane_loads_b32", "shared_miss_paths"]
         return {n: int(v) for n, v in zip(names, c)}
 
     def kernel_stats(self, reset: bool = False):
@@ -403,6 +403,14 @@ class VRendererHIP:
         check(self._lib.vrhip_kernel_stats(self._need_ctx(), ctypes.byref(ms), ctypes.byref(n), int(reset)),
               "vrhip_kernel_stats")
         return float(ms.value), int(n.value)
+
+    def last_launch_info(self) -> dict:
+        """Shape of the last production launch (vrhip_last_launch_info)."""
+        sp, us, kd = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        check(self._lib.vrhip_last_launch_info(self._need_ctx(), ctypes.byref(sp), ctypes.byref(us), ctypes.byref(kd)),
+              "vrhip_last_launch_info")
+        return {"split": int(sp.value), "use_scratch": int(us.value),
+                "kind": ("render_kernel", "path_pool", "service")[min(int(kd.value), 2)]}
 
     def device_buffers(self):
         a, r, d = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
