@@ -48,6 +48,23 @@ int vrhip_device_count(int *count);
  * float4[W*H] accumulation buffer and the RGBA8 colour/depth images on
  * `device`, zero-fills, frame counter = 1.  1 <= width, height <= 65535. */
 int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx **out);
+/* One renderer over several GPUs of this process (SURVEY 8(b) "create_multi";
+ * no reference counterpart: the reference's caller creates one renderer,
+ * src/NGLScene.cpp:82-89).  A member context per device in `devices` (no
+ * repeats), each rendering the 16x16 tiles i, i + n, ... of the image; the
+ * RCCL communicators are made in one call (ncclCommInitAll).  The returned
+ * context is the lead (devices[0]): every setting and upload on it fans out
+ * to all members; vrhip_render renders every device's tiles and gathers the
+ * RGBA8 and depth tiles to the lead (one grouped ncclGather each), so the
+ * lead's images, read-back and GL presentation show the whole frame;
+ * vrhip_read_accum gathers the accumulation first; vrhip_comm_gather gathers
+ * the given image.  Refused on it: vrhip_set_tiling, vrhip_set_stream,
+ * vrhip_comm_init/destroy, vrhip_set_service, the counting renders.  n = 1 is
+ * allowed (the same code, a one-rank communicator). */
+int vrhip_create_multi(const int *devices, uint32_t n_devices, uint32_t width, uint32_t height, vrhip_ctx **out);
+/* The devices of a context (one for vrhip_create, the group for
+ * vrhip_create_multi, lead first); `devices` may be NULL (count only). */
+int vrhip_device_group(vrhip_ctx *ctx, uint32_t *n_devices, int *devices);
 /* replaces vRendererCuda::cleanUp + cu_cleanUp (src/vRendererCuda.cpp:167-199,
  * cuda/src/PathTracer.cu:1009-1030). NULL is a no-op. */
 int vrhip_destroy(vrhip_ctx *ctx);
@@ -205,6 +222,23 @@ int vrhip_set_path_split(vrhip_ctx *ctx, uint32_t groups);
  * than 2^25 on a tiled rank (small or sharded frames, where the drain of a
  * launch is a large share of it). */
 int vrhip_set_overlap(vrhip_ctx *ctx, int mode);
+/* Render service (no reference counterpart: a scheduling mode; results are
+ * unchanged bit for bit).  Consecutive vrhip_render calls of a mesh scene run
+ * as one session on ONE persistent kernel: each launch is posted to a
+ * descriptor ring the running kernel reads, so the drain of a launch (its
+ * last, longest paths) overlaps the next launch's paths instead of ending a
+ * kernel.  The images are summed, in path order, by one finish pass when the
+ * session closes: at the next call on the context that is not vrhip_render or
+ * vrhip_comm_gather (sync, read-back, upload, any setting, ...), when its 32
+ * launch slots are used, or when a launch does not fit it (another scene,
+ * camera or tiling, more frames than its slots hold).  vrhip_comm_gather
+ * inside a session gathers the image as of that call when the session closes.
+ * mode 1: every production mesh launch; 0: never; -1 (default, also
+ * VRHIP_SERVICE): launches that overlap on the path streams (fewer than 2^24
+ * paths, or 2^25 on a tiled rank) when the previous launch is still in flight
+ * -- unsynchronised back-to-back calls, not the first call of a burst.  The
+ * open session's kernel retires after 20 ms without a new launch. */
+int vrhip_set_service(vrhip_ctx *ctx, int mode);
 /* Frames rendered since the last clear (vRendererCuda::getFrameCount,
  * include/vRendererCuda.h:124). */
 int vrhip_frame_count(vrhip_ctx *ctx, uint32_t *frames);

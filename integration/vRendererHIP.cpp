@@ -38,6 +38,29 @@ vRendererHIP::~vRendererHIP()
   cleanUp();
 }
 
+std::vector<int> vRendererHIP::parseDevices(const char *_list)
+{
+  // "0,1,2,3" (commas or spaces); anything that is not a device index ends the list
+  std::vector<int> out;
+  if(!_list)
+    return out;
+  const char *p = _list;
+  while(*p)
+  {
+    while(*p == ',' || *p == ' ')
+      ++p;
+    if(!*p)
+      break;
+    char *end = nullptr;
+    const long v = std::strtol(p, &end, 10);
+    if(end == p || v < 0 || v > 1023)
+      break;
+    out.push_back(static_cast<int>(v));
+    p = end;
+  }
+  return out;
+}
+
 void vRendererHIP::validate(int _status, const std::string &_msg)
 {
   if(_status == VRHIP_OK)
@@ -57,8 +80,19 @@ void vRendererHIP::init(const unsigned int &_w, const unsigned int &_h)
 {
   m_width = _w;
   m_height = _h;
-  const char *dev = std::getenv("VRHIP_DEVICE");
-  validate(vrhip_create(dev ? std::atoi(dev) : 0, _w, _h, &m_ctx), "Create HIP context");
+  // VRHIP_DEVICES="0,1,2,3": one renderer over those GPUs (the image's tiles
+  // dealt over them, gathered to the first over RCCL every frame); else one
+  // GPU, VRHIP_DEVICE (default 0)
+  const std::vector<int> devices = parseDevices(std::getenv("VRHIP_DEVICES"));
+  if(devices.size() > 1)
+    validate(vrhip_create_multi(devices.data(), static_cast<uint32_t>(devices.size()), _w, _h, &m_ctx),
+             "Create multi-GPU HIP context");
+  else
+  {
+    const char *dev = std::getenv("VRHIP_DEVICE");
+    validate(vrhip_create(devices.size() == 1 ? devices[0] : (dev ? std::atoi(dev) : 0), _w, _h, &m_ctx),
+             "Create HIP context");
+  }
   validate(vrhip_set_fresnel(m_ctx, m_fresnelCoef, m_fresnelPow), "Set Fresnel parameters");
   m_rgba.assign(static_cast<size_t>(_w) * _h * 4, 0);
   m_depth.assign(static_cast<size_t>(_w) * _h * 4, 0);

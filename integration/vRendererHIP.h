@@ -48,6 +48,9 @@ public:
   /// Flattens the application's SBVH (vMeshData::m_bvh) into that layout, as
   /// initMesh uploads it; false for an empty tree or a leaf root.  Host only.
   static bool flattenSBVH(const vMeshData &_meshData, FlatMesh &_out);
+  /// VRHIP_DEVICES parsing ("0,1,2,3"): the GPUs init() spreads the image
+  /// over (vrhip_create_multi) when it names more than one.  Host only.
+  static std::vector<int> parseDevices(const char *_list);
 
 private:
   /// Reference error behaviour (src/vRendererCuda.cpp:454-467): message,

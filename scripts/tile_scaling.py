@@ -35,6 +35,8 @@ px = (W // 16) * 16 * (H // 16) * 16
 r = VRendererHIP(0)
 scenes.load_into(r, sc)
 r.set_path_split(SPLIT)
+if os.environ.get("TS_SERVICE"):          # experiments: vrhip_set_service mode (1 always, 0 never, -1 automatic)
+    r.set_service(int(os.environ["TS_SERVICE"]))
 if os.environ.get("TS_OVERLAP"):          # experiments: vrhip_set_overlap mode (1 always, 0 never, -1 automatic)
     r.set_overlap(int(os.environ["TS_OVERLAP"]))
 base = None

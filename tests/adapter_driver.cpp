@@ -286,10 +286,22 @@ static int runSceneFile(const char *_out, const char *_scene)
 //        adapter_driver <out> --scene <file>       a scene file (above) through every ingestion call
 //        adapter_driver <out> <mesh> [--flatten]   Cornell + the mesh (its SBVH flattened by the
 //                                                  adapter); --flatten: only write the flat arrays (no GPU)
+//        adapter_driver <out> --devices <list>     write the device list init() parses from VRHIP_DEVICES (no GPU)
 int main(int argc, char **argv)
 {
   if(argc < 2)
     return 2;
+  if(argc >= 4 && std::strcmp(argv[2], "--devices") == 0)
+  {
+    const std::vector<int> d = vRendererHIP::parseDevices(argv[3]);
+    FILE *out = std::fopen(argv[1], "w");
+    if(!out)
+      return 4;
+    for(size_t i = 0; i < d.size(); ++i)
+      std::fprintf(out, i ? ",%d" : "%d", d[i]);
+    std::fclose(out);
+    return 0;
+  }
   if(argc >= 4 && std::strcmp(argv[2], "--scene") == 0)
     return runSceneFile(argv[1], argv[3]);
   vMeshData mesh;

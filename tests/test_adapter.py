@@ -34,6 +34,17 @@ def test_adapter_compiles_and_links(native, tmp_path):
     assert os.path.exists(exe)
 
 
+@pytest.mark.parametrize("spec,want", [("0,1,2,3", "0,1,2,3"), ("2 5", "2,5"), ("7", "7"), ("", ""),
+                                       ("1,x,3", "1"), (",,4,", "4")])
+def test_adapter_parses_device_list(native, tmp_path, spec, want):
+    """VRHIP_DEVICES as init() reads it: more than one device selects the
+    multi-GPU context (vrhip_create_multi), one device or none a single one."""
+    exe = _build_driver(tmp_path)
+    out = str(tmp_path / "devs.txt")
+    subprocess.run([exe, out, "--devices", spec], check=True, capture_output=True, timeout=60)
+    assert open(out).read() == want
+
+
 def _write_mesh(path, mesh):
     with open(path, "wb") as f:
         f.write(np.array([len(mesh["positions"]), len(mesh["tris"])], np.uint32).tobytes())

@@ -324,3 +324,17 @@ def test_load_exr_rejects_unsupported(native, tmp_path):
     (tmp_path / "junk.exr").write_bytes(b"not an exr file at all")
     with pytest.raises(_native.VRHIPError):
         load_exr(tmp_path / "junk.exr")
+
+
+def test_create_multi_rejects_bad_device_lists(native):
+    """vrhip_create_multi checks its device list before touching a GPU: no
+    devices, a NULL list, a repeated device, more than 64 are refused."""
+    import ctypes
+    ctx = ctypes.c_void_p(None)
+    for devs in ([], [0, 0], [1, 2, 1]):
+        arr = (ctypes.c_int * max(len(devs), 1))(*devs)
+        assert native.vrhip_create_multi(arr, len(devs), 64, 64, ctypes.byref(ctx)) == -1
+        assert not ctx.value
+    assert native.vrhip_create_multi(None, 2, 64, 64, ctypes.byref(ctx)) == -1
+    arr = (ctypes.c_int * 65)(*range(65))
+    assert native.vrhip_create_multi(arr, 65, 64, 64, ctypes.byref(ctx)) == -1

@@ -126,3 +126,77 @@ def test_bench_two_ranks_gloo_rehearsal(native):
     assert abs(st["efficiency"] - st["value"] / (2 * st["one_gpu_value"])) < 1e-3
     # kernel time is the union of overlapping launch spans: never more than the step
     assert out["roofline"]["avg_launch_ms"] <= out["ms_per_step"] * 1.001
+
+
+def _single(sc, frames, times):
+    from vrenderer_pathtracer_amd import VRendererHIP, scenes
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.render(frames=frames, times=times)
+    out = r.read_accum(), r.read_rgba8(), r.read_depth8()
+    r.cleanUp()
+    return out
+
+
+def _multi(sc, devices, calls, t0):
+    from vrenderer_pathtracer_amd import VRendererHIP, scenes
+    r = VRendererHIP(list(devices))
+    scenes.load_into(r, sc)
+    assert r.device_group() == list(devices)
+    t = t0
+    for n in calls:
+        r.render(frames=n, times=[t + k for k in range(n)])
+        t += n
+    out = r.read_accum(), r.read_rgba8(), r.read_depth8(), r.getFrameCount()
+    r.cleanUp()
+    return out
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_multi_context_one_device_bitexact(native, oracle, cfg):
+    """vrhip_create_multi with one device runs the multi-GPU code (fan-out of
+    every setting and upload, per-device render, grouped RCCL gathers of
+    RGBA8 / depth / accum to the lead over a one-rank communicator): equal to
+    the plain context and to the oracle bit for bit."""
+    import pyoracle as po
+    from vrenderer_pathtracer_amd import scenes
+    sc = scenes.make_scene(cfg, 96, 64)
+    t = sc["time"]
+    ga, gr, gd, nf = _multi(sc, [0], [2, 1], t)
+    assert nf == 3
+    sa, sr, sd = _single(sc, 3, [t, t + 1, t + 2])
+    assert np.array_equal(ga.view(np.uint32), sa.view(np.uint32))
+    assert np.array_equal(gr, sr) and np.array_equal(gd, sd)
+    oa, orgba, _, _ = po.render(sc, frames=3, times=[t, t + 1, t + 2], libm=po.LIBM_PORTABLE)
+    H, W = 64, 96
+    assert np.array_equal(ga[:H, :W].view(np.uint32), oa[:H, :W].view(np.uint32))
+    assert np.array_equal(gr[:H, :W], orgba[:H, :W])
+
+
+def test_multi_context_refuses_per_rank_calls(native):
+    """Tiling, streams, communicators and the render service belong to the
+    multi-device context itself: setting them on it is refused."""
+    from vrenderer_pathtracer_amd import VRendererHIP, scenes
+    from vrenderer_pathtracer_amd._native import VRHIPError
+    sc = scenes.make_scene("C2", 64, 64)
+    r = VRendererHIP([0])
+    scenes.load_into(r, sc)
+    for call in (lambda: r.set_tiling(0, 2), lambda: r.set_service(1)):
+        with pytest.raises(VRHIPError):
+            call()
+    r.cleanUp()
+
+
+def test_multi_context_two_devices_bitexact(native):
+    """Two GPUs behind one context: each renders half the tiles, RCCL gathers
+    them to the first; the images equal the one-GPU render bit for bit."""
+    from vrenderer_pathtracer_amd import device_count
+    if device_count() < 2:
+        pytest.skip("needs 2 GPUs (one process drives both)")
+    from vrenderer_pathtracer_amd import scenes
+    sc = scenes.make_scene("C3", 160, 96)
+    t = sc["time"]
+    ga, gr, gd, _ = _multi(sc, [0, 1], [2, 2], t)
+    sa, sr, sd = _single(sc, 4, [t + k for k in range(4)])
+    assert np.array_equal(ga.view(np.uint32), sa.view(np.uint32))
+    assert np.array_equal(gr, sr) and np.array_equal(gd, sd)

@@ -1,0 +1,154 @@
+"""Render service sessions (vrhip_set_service): consecutive render calls run
+on ONE persistent kernel fed from a descriptor ring, their results summed in
+path order by one finish pass when the session closes.  Bar: bit-identical
+to launch-by-launch rendering (vrhip_set_service(0)) and to the oracle
+(portable libm), whatever the session boundaries."""
+import time
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from vrenderer_pathtracer_amd import VRendererHIP, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(sc, calls, service, tiling=None, overlap=None, sleeps=None):
+    """calls: list of frame counts per render call (async); returns accum,
+    rgba, depth, frame count and the last launch's kind."""
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.set_service(service)
+    if overlap is not None:
+        r.set_overlap(overlap)
+    if tiling:
+        r.set_tiling(*tiling)
+    t = sc["time"]
+    kinds = []
+    for i, n in enumerate(calls):
+        r.render(frames=n, times=[t + k for k in range(n)], sync=False)
+        kinds.append(r.last_launch_info()["kind"])
+        t += n
+        if sleeps and i in sleeps:
+            time.sleep(sleeps[i])
+    out = r.read_accum(), r.read_rgba8(), r.read_depth8(), r.getFrameCount()
+    r.cleanUp()
+    return out, kinds
+
+
+def _eq(a, b, what):
+    if a.dtype == np.float32:
+        d = (a.view(np.uint32) != b.view(np.uint32)).any(-1)
+    else:
+        d = (a != b).any(-1)
+    assert int(d.sum()) == 0, f"{what}: {int(d.sum())} pixels differ"
+
+
+@pytest.mark.parametrize("cfg,w,h", [("C2", 96, 64), ("C3", 96, 64), ("C5", 96, 64)])
+def test_service_session_equals_launch_by_launch_and_oracle(native, oracle, cfg, w, h):
+    """Seven async calls of 1-4 frames in one session (the first opens it:
+    service mode 1) equal the same calls without the service and the oracle's
+    frame-by-frame loop, bit for bit (accum, RGBA8, depth)."""
+    sc = scenes.make_scene(cfg, w, h)
+    calls = [2, 1, 4, 1, 3, 2, 1]
+    (a1, r1, d1, n1), k1 = _run(sc, calls, 1)
+    (a0, r0, d0, n0), k0 = _run(sc, calls, 0)
+    assert set(k1) == {"service"} and "service" not in k0
+    assert n1 == n0 == sum(calls)
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8"); _eq(d1, d0, "depth8")
+    times = [sc["time"] + k for k in range(sum(calls))]
+    oa, orgba, od, _ = po.render(sc, frames=sum(calls), times=times, libm=po.LIBM_PORTABLE)
+    H, W = (h // 16) * 16, (w // 16) * 16
+    _eq(a1[:H, :W], oa[:H, :W], "accum vs oracle")
+    _eq(r1[:H, :W], orgba[:H, :W], "rgba8 vs oracle")
+    _eq(d1[:H, :W], od[:H, :W], "depth8 vs oracle")
+
+
+def test_service_session_limits(native, oracle):
+    """Sessions close and reopen on their own: 40 one-frame calls (more than
+    the 32 launch slots), a call of more frames than the session's slots hold
+    (4 after 1-frame launches), a 70-frame call (two launches of 64 + 6).
+    Bit-identical to launch-by-launch rendering."""
+    sc = scenes.make_scene("C3", 64, 48)
+    calls = [1] * 40 + [4, 1, 70, 2]
+    (a1, r1, _, n1), _ = _run(sc, calls, 1)
+    (a0, r0, _, n0), _ = _run(sc, calls, 0)
+    assert n1 == n0 == sum(calls)
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8")
+
+
+def test_service_automatic_mode_and_tiling(native):
+    """Automatic mode on a tiled rank: the first call of a burst runs as
+    usual, the calls behind it (launch in flight) join a session; scene changes
+    (Fresnel) and host pauses longer than the post window (5 ms) and than the
+    kernel's idle limit (20 ms) start new sessions.  Bit-identical to
+    launch-by-launch rendering."""
+    sc = scenes.make_scene("C3")              # 1280x720: a 2-frame shard launch outlasts the host's next call
+    calls = [2] * 6
+    (a1, r1, d1, _), k1 = _run(sc, calls, -1, tiling=(1, 3), sleeps={2: 0.008, 4: 0.05})
+    (a0, r0, d0, _), _ = _run(sc, calls, 0, tiling=(1, 3))
+    assert "service" in k1, k1
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8"); _eq(d1, d0, "depth8")
+
+    def with_changes(service):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_service(service)
+        t = sc["time"]
+        for i in range(3):
+            r.render(frames=2, times=[t + 2 * i, t + 2 * i + 1], sync=False)
+        r.setFresnelCoef(0.35)                 # another launch parameter: a new session
+        for i in range(3, 6):
+            r.render(frames=2, times=[t + 2 * i, t + 2 * i + 1], sync=False)
+        r.set_tiling(0, 2)
+        r.render(frames=1, times=[t + 12], sync=False)
+        r.render(frames=1, times=[t + 13], sync=False)
+        out = r.read_accum(), r.read_rgba8()
+        r.cleanUp()
+        return out
+    (ca, cr), (ba, br) = with_changes(1), with_changes(0)
+    _eq(ca, ba, "accum with scene changes"); _eq(cr, br, "rgba8 with scene changes")
+
+
+def test_service_deferred_gather_single_rank(native):
+    """vrhip_comm_gather inside a session (one-rank RCCL communicator): the
+    gathers are deferred to the session's close; the gathered image and the
+    accumulation equal the launch-by-launch render."""
+    from vrenderer_pathtracer_amd.renderer import comm_unique_id
+    from vrenderer_pathtracer_amd.tiles import WHAT_ACCUM, WHAT_RGBA8
+    sc = scenes.make_scene("C2", 96, 64)
+
+    def run(service):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_service(service)
+        r.comm_init(0, 1, comm_unique_id())
+        t = sc["time"]
+        for i in range(5):
+            r.render(frames=2, times=[t + 2 * i, t + 2 * i + 1], sync=False)
+            r.comm_gather(WHAT_RGBA8)
+            if i == 3:
+                r.comm_gather(WHAT_ACCUM)
+        r.sync()
+        out = r.read_accum(), r.read_rgba8(), r.read_depth8()
+        r.comm_destroy()
+        r.cleanUp()
+        return out
+    got, base = run(1), run(0)
+    for g, b, what in zip(got, base, ("accum", "rgba8", "depth8")):
+        _eq(g, b, what)
+
+
+def test_service_kernel_stats_count_every_launch(native):
+    """The session's kernel span is accounted once for all its launches."""
+    sc = scenes.make_scene("C2", 64, 64)
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.set_service(1)
+    r.kernel_stats(reset=True)
+    for i in range(5):
+        r.render(frames=1, times=[sc["time"] + i], sync=False)
+    ms, n = r.kernel_stats()
+    r.cleanUp()
+    assert n == 5 and ms > 0.0

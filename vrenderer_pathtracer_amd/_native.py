@@ -37,6 +37,9 @@ _SIGNATURES = {
     "vrhip_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "vrhip_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_ctx)]),
     "vrhip_destroy": (ctypes.c_int, [_ctx]),
+    "vrhip_create_multi": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.POINTER(_ctx)]),
+    "vrhip_device_group": (ctypes.c_int, [_ctx, _u32, ctypes.POINTER(ctypes.c_int)]),
     "vrhip_set_stream": (ctypes.c_int, [_ctx, _vp]),
     "vrhip_get_stream": (_vp, [_ctx]),
     "vrhip_set_camera": (ctypes.c_int, [_ctx, _f, _f, _f, _f, ctypes.c_float]),
@@ -87,6 +90,7 @@ _SIGNATURES = {
     "vrhip_comm_destroy": (ctypes.c_int, [_ctx]),
     "vrhip_last_kernel_ms": (ctypes.c_int, [_ctx, _f]),
     "vrhip_last_launch_info": (ctypes.c_int, [_ctx, _u32, _u32, _u32]),
+    "vrhip_set_service": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "vrhip_bvh_info": (ctypes.c_int, [_ctx, _u32, _u32, _u32]),
     "vrhip_selftest_math": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _f, _f, _f, ctypes.c_size_t]),
     "vrhip_selftest_rcp": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,

@@ -61,7 +61,8 @@ def _jobs() -> int:
 def build(force: bool = False, verbose: bool = False, extra_flags=None, out_path: str = None) -> str:
     """Compile every source to an object in parallel (hipcc -c), then link
     libvrhip.so.  extra_flags / out_path: variant builds (scripts/build_variants.sh)."""
-    out = out_path or LIB_PATH
+    out = os.path.abspath(out_path or LIB_PATH)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     if not force and out_path is None and not needs_build():
         return LIB_PATH
     import concurrent.futures

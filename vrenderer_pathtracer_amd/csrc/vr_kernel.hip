@@ -150,12 +150,13 @@ __global__ void selftest_math_kernel(int fn, const float* a, const float* b, flo
 static void launch_scene(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec)
 {
     const uint32_t need = p.flags & kFeatAll;
-    if (need == kFeatCornellMesh) launch_spec_c2(p, n_tiles, stack_depth, s, exec);
-    else if (need == kFeatCornellSphere) launch_spec_c1(p, n_tiles, stack_depth, s, exec);
-    else if (need == kFeatHdriMesh) launch_spec_c5(p, n_tiles, stack_depth, s, exec);
-    else if (need == kFeatHdriMeshTex) launch_spec_c3(p, n_tiles, stack_depth, s, exec);
-    else if (need == kFeatHdriBrdfSphere) launch_spec_c4(p, n_tiles, stack_depth, s, exec);
-    else launch_spec_generic(p, n_tiles, stack_depth, s, exec);
+    const int mode = exec ? 1 : 0;
+    if (need == kFeatCornellMesh) launch_spec_c2(p, n_tiles, stack_depth, s, mode);
+    else if (need == kFeatCornellSphere) launch_spec_c1(p, n_tiles, stack_depth, s, mode);
+    else if (need == kFeatHdriMesh) launch_spec_c5(p, n_tiles, stack_depth, s, mode);
+    else if (need == kFeatHdriMeshTex) launch_spec_c3(p, n_tiles, stack_depth, s, mode);
+    else if (need == kFeatHdriBrdfSphere) launch_spec_c4(p, n_tiles, stack_depth, s, mode);
+    else launch_spec_generic(p, n_tiles, stack_depth, s, mode);
 }
 
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int count, void* stream)
@@ -166,6 +167,78 @@ int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int 
     if (count == 1) launch_counting(p, blocks, stack_depth, s);   // the reference algorithm's event counts
     else if (stack_depth > 32) launch_spec_deep(p, n_tiles, s, count != 0);
     else launch_scene(p, n_tiles, stack_depth, s, count == 2);
+    return (int)hipGetLastError();
+}
+
+// The render service's session finish pass: per pixel, every launch's path
+// results summed in path order launch by launch (the float4 operations of
+// finish_kernel, so the accumulation equals frame-by-frame rendering bit for
+// bit), the launch's images staged for a deferred gather where one was
+// requested (vrhip_comm_gather inside a session), and the final accum /
+// RGBA8 / depth.  Staged images are packed like pack_tiles_kernel: owned
+// tile j's pixels at [256 j, 256 j + 256), row-major within the tile.
+__global__ void __launch_bounds__(kBlockThreads) svc_finish_kernel(const RenderParams p, const SvcFinish f)
+{
+    const uint32_t tile = blockIdx.x, tid = threadIdx.x;
+    const int wave = (int)tid >> 6, lane = (int)tid & 63;
+    const uint32_t gtile = p.rank + tile * p.nranks;
+    const uint32_t tile_y = gtile / p.tiles_x;
+    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t lx = (uint32_t)((wave & 1) * 8 + (lane & 7)), ly = (uint32_t)((wave >> 1) * 8 + (lane >> 3));
+    const uint32_t x = tile_x * 16u + lx, y = tile_y * 16u + ly;
+    if (x >= p.wr || y >= p.hr) return;
+    const uint32_t ind = x + y * p.W;
+    const uint32_t slot = tile * kBlockThreads + tid;
+    const uint32_t packed = tile * 256u + ly * 16u + lx;
+    vr4 io = f.first_frame != 1u ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
+    const bool cornell = (p.flags & F_CORNELL) != 0u;
+    uint32_t frame = f.first_frame;
+    float last_w = 0.f;
+    for (uint32_t L = 0; L < f.n; ++L) {
+        const vr3* base = reinterpret_cast<const vr3*>(reinterpret_cast<const uint8_t*>(p.paths) + (size_t)L * p.svc_slot_bytes);
+        const float depth = reinterpret_cast<const float*>(base + (size_t)2u * p.svc_kmax * p.path_stride)[slot];
+        const vr3* src = base + slot;
+        const uint32_t n_paths = 2u * f.n_frames[L];
+        for (uint32_t q = 0; q < n_paths; ++q) {
+            const vr3 r = src[(size_t)q * p.path_stride];
+            last_w = (cornell && escaped(r.x)) ? 0.f : depth;
+            io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
+        }
+        frame += f.n_frames[L];
+        if (f.gather[L]) {
+            uint8_t* st = f.staging + (size_t)L * f.stage_bytes;
+            if (f.gather[L] & 1u) reinterpret_cast<u8x4*>(st)[packed] = tonemap(io, frame - 1u);
+            if (f.gather[L] & 4u) {
+                const unsigned char db = f2u8((1.f - last_w) * 255);
+                u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
+                reinterpret_cast<u8x4*>(st + (size_t)4u * f.stage_pixels)[packed] = dv;
+            }
+            if (f.gather[L] & 2u) reinterpret_cast<vr4*>(st + (size_t)8u * f.stage_pixels)[packed] = io;
+        }
+    }
+    const unsigned char db = f2u8((1.f - last_w) * 255);
+    u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
+    p.depth[ind] = dv;
+    p.rgba[ind] = tonemap(io, frame - 1u);
+    p.accum[ind] = io;
+}
+
+int launch_service(const RenderParams& p, uint32_t n_tiles, int stack_depth, void* stream)
+{
+    if (n_tiles == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t need = p.flags & kFeatAll;
+    if (need == kFeatCornellMesh) launch_spec_c2(p, n_tiles, stack_depth, s, 2);
+    else if (need == kFeatHdriMesh) launch_spec_c5(p, n_tiles, stack_depth, s, 2);
+    else if (need == kFeatHdriMeshTex) launch_spec_c3(p, n_tiles, stack_depth, s, 2);
+    else launch_spec_generic(p, n_tiles, stack_depth, s, 2);
+    return (int)hipGetLastError();
+}
+
+int launch_service_finish(const RenderParams& p, const SvcFinish& f, uint32_t n_tiles, void* stream)
+{
+    if (n_tiles == 0 || f.n == 0) return 0;
+    hipLaunchKernelGGL(svc_finish_kernel, dim3(n_tiles), dim3(kBlockThreads), 0, (hipStream_t)stream, p, f);
     return (int)hipGetLastError();
 }
 

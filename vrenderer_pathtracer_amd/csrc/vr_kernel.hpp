@@ -1366,7 +1366,7 @@ constexpr bool cornell_kernel() {
     // kernels (F_SMALL), which spilled 19 VGPRs at 7 with helper lanes and
     // cost counting (8-rank C2 shard step 1.317 -> 1.257 ms at 6, r03p)
     return (FEAT & F_EXACT) != 0u && (FEAT & F_CORNELL) != 0u && (FEAT & F_INLINE_PRIM) == 0u &&
-           (FEAT & F_SMALL) == 0u;
+           (FEAT & (F_SMALL | F_SERVICE)) == 0u;
 }
 
 #ifndef VR_XCD_BANDS
@@ -1652,6 +1652,300 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     if (CNT) flush_counts(p, cnt, lane, true);
 }
 
+// ---- render service ---------------------------------------------------------
+// A session (vrhip_api.cpp) runs consecutive render launches on ONE
+// persistent kernel: the drain of launch L -- its last, longest paths, a
+// large share of a short launch (a 16-frame C3 shard of 3.7 M paths is
+// ~280 us of work next to a ~300-400 us longest path) --
+// overlaps launch L+1's paths instead of ending a kernel.  The host appends
+// launch descriptors (first frame, frame count, per-frame seeds) to a ring in
+// host-pinned memory; the ring wave mirrors them into device memory; every
+// other wave takes chunks of (sub-tile, path) of launch L, then of L+1, ...,
+// exactly as render_wave_kernel does for one launch.  A session's camera,
+// scene and tiling are fixed (the host closes it on any change), so the
+// camera rays' closest hits are the same for all its launches: primary_kernel
+// traces them once when the session opens, and every path of every launch
+// starts from them.  Results go to the launch's scratch slot; the session
+// finish pass (svc_finish_kernel) sums every pixel's paths launch by launch in
+// path order, so the image is the reference's bit for bit whatever the
+// interleaving.
+__device__ __forceinline__ uint32_t svc_ld(const uint32_t* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// a path's radiance into its launch's slot (the store_path layout per slot)
+__device__ __forceinline__ void svc_store_path(const RenderParams& p, uint32_t L, uint32_t q, uint32_t slot,
+                                               const vr4& out, float depth)
+{
+    vr3* const base = reinterpret_cast<vr3*>(reinterpret_cast<uint8_t*>(p.paths) + (size_t)L * p.svc_slot_bytes);
+    base[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
+    if (q == 0u) reinterpret_cast<float*>(base + (size_t)2u * p.svc_kmax * p.path_stride)[slot] = depth;
+}
+
+// The ring wave (the last wave of block 0; it takes no paths): mirrors the
+// host ring into device memory every ~1 us -- newly posted descriptors (sc1
+// stores, drained, then the control word), the host's close, or, after
+// svc_idle_ticks without a new launch, the session's retirement -- until
+// the session is closed.  The host writes `closed` only after its last post
+// and this reads `closed` before `posted`, so a close carries the final count.
+__device__ __forceinline__ void svc_ring_wave(const RenderParams& p, int lane)
+{
+    SvcDevCtl* const d = p.svc_dev;
+    uint32_t dp = 0, last = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        uint32_t hc = 0, hp = 0;
+        if (lane == 0) {
+            hc = __hip_atomic_load(&p.svc_host->closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            hp = __hip_atomic_load(&p.svc_host->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        hc = __builtin_amdgcn_readfirstlane(hc);
+        hp = __builtin_amdgcn_readfirstlane(hp);
+        if (hp > kSvcMaxLaunches) hp = kSvcMaxLaunches;
+        const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        if (hp > dp) {
+            for (uint32_t k = dp; k < hp; ++k) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(&p.svc_host->desc[k]);
+                uint32_t* dst = reinterpret_cast<uint32_t*>(&d->desc[k]);
+                for (uint32_t w = (uint32_t)lane; w < kSvcLaunchWords; w += 64u) {
+                    const uint32_t v = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(dst + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) atomicMax(&d->ctl, hp | (hc ? kSvcClosed : 0u));
+            dp = hp;
+            last = now;
+            if (hc) return;
+        } else if (hc != 0u || now - last > p.svc_idle_ticks) {
+            if (lane == 0) atomicMax(&d->ctl, dp | kSvcClosed);    // closed by the host, or retired when idle
+            return;
+        }
+        __builtin_amdgcn_s_sleep(32);
+    }
+}
+
+template <int STACK, uint32_t FEAT, int BT>
+__device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L)
+{
+    const int tid = (int)threadIdx.x;
+    const int lane = tid & 63;
+#if VR_X != 1
+    if (blockIdx.x == 0u && (tid >> 6) == BT / 64 - 1) { svc_ring_wave(p, lane); return; }
+#endif
+    const uint32_t n_sub = p.path_stride >> 6;             // 8x8 sub-tiles of the rank's tiles
+    Cnt cnt;
+    const uint32_t Q = p.n_queues;
+    const uint32_t q0 = blockIdx.x & (Q - 1u);
+    uint32_t qj = q0;
+    __shared__ unsigned long long lds_dead[BT / 64];
+    unsigned long long* const my_dead = lds_dead + (tid >> 6);
+    if (lane == 0) *my_dead = 0ull;
+    // per wave, in LDS (read at grabs only; the kernel is at its register
+    // limits): the launch sL this wave takes chunks from, the launches it
+    // knows to be posted, launch sL's frame count
+    struct Ring { uint32_t sL, posted, l_nf; };
+    __shared__ Ring lds_ring[BT / 64];
+    Ring* const rg = lds_ring + (tid >> 6);
+    if (lane == 0) *rg = Ring{ 0u, 0u, 0u };
+    enum { GOT = 0, WAIT = 1, DONE = 2 };
+    // the seeds' frame base (first frame + frame) and time of the chunks the
+    // wave hands out -- the current one and the next one -- in LDS (cslot:
+    // which of the two records is the current chunk's)
+    __shared__ uint32_t lds_seed[BT / 64][2][2];
+    uint32_t (*const seed)[2] = lds_seed[tid >> 6];
+    uint32_t cslot = 0;
+    // next chunk (wave-uniform) into seed record `rec`: sub-tile, path and
+    // launch; GOT, WAIT (the ring holds nothing more yet) or DONE (the session
+    // is closed and drained)
+    auto grab = [&](uint32_t& sub, uint32_t& path, uint32_t& lc, uint32_t rec) -> int {
+        uint32_t sL = __builtin_amdgcn_readfirstlane(rg->sL), posted = __builtin_amdgcn_readfirstlane(rg->posted);
+        uint32_t l_nf = __builtin_amdgcn_readfirstlane(rg->l_nf);
+        for (;;) {
+            if (sL >= posted) {
+                uint32_t c = 0;
+                if (lane == 0) c = svc_ld(&p.svc_dev->ctl);
+                c = __builtin_amdgcn_readfirstlane(c);
+                posted = c & ~kSvcClosed;
+                if (sL >= posted) {
+                    if (lane == 0) { rg->sL = sL; rg->posted = posted; rg->l_nf = l_nf; }
+                    sub = ~0u;
+                    return (c & kSvcClosed) ? DONE : WAIT;
+                }
+            }
+            if (l_nf == 0u) {
+                uint32_t nf = 0;
+                if (lane == 0) nf = svc_ld(&p.svc_dev->desc[sL].n_frames);
+                l_nf = __builtin_amdgcn_readfirstlane(nf);
+                if (l_nf == 0u || l_nf > p.svc_kmax) l_nf = 1u;   // (never: the host posts 1..svc_kmax frames)
+            }
+            const uint32_t np = 2u * l_nf;
+            uint32_t* const heads = p.svc_qctl + (size_t)sL * kSvcQctlWords;
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(heads + qj * kQueueStride, 1u);
+            v = __builtin_amdgcn_readfirstlane(v);
+            uint32_t pth;
+            const uint32_t sb = queue_item(qj, v, Q, np, pth);
+            if (sb < n_sub) {
+                if (lane == 0) {
+                    rg->sL = sL; rg->posted = posted; rg->l_nf = l_nf;
+                    seed[rec][0] = svc_ld(&p.svc_dev->desc[sL].first_frame) + (pth >> 1);
+                    seed[rec][1] = svc_ld(&p.svc_dev->desc[sL].times[pth >> 1]);
+                }
+                sub = sb; path = pth; lc = sL;
+                return GOT;
+            }
+            // queue qj of launch sL is drained: the drained-queue mask of the
+            // small launches (render_wave_kernel grab)
+            uint32_t m0 = 0, m1 = 0;
+            if (lane == 0) {
+                unsigned long long* const dmask = queue_drained_mask(heads);
+                uint32_t pq;
+                const bool first = v == 0u || queue_item(qj, v - 1u, Q, np, pq) < n_sub;
+                const unsigned long long m = first ? atomicOr(dmask, 1ull << qj)
+                                                   : __hip_atomic_load(dmask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long dd = *my_dead | m | (1ull << qj);
+                *my_dead = dd;
+                m0 = (uint32_t)dd; m1 = (uint32_t)(dd >> 32);
+            }
+            const unsigned long long live = all_q_of(Q) & ~(((unsigned long long)__builtin_amdgcn_readfirstlane(m1) << 32) |
+                                                             (unsigned long long)__builtin_amdgcn_readfirstlane(m0));
+            if (live == 0ull) {                            // launch sL is out of work: the next one
+                ++sL;
+                l_nf = 0u;
+                if (lane == 0) *my_dead = 0ull;
+                qj = q0;
+                continue;
+            }
+            const unsigned long long after = qj + 1u < 64u ? (live >> (qj + 1u)) << (qj + 1u) : 0ull;
+            qj = (uint32_t)__builtin_ctzll(after != 0ull ? after : live);
+        }
+    };
+    int ring = WAIT;                                       // the status of the last grab
+    uint32_t cur_sub = ~0u, cur_q = 0, cur_L = 0;
+    uint32_t next = 64u;                                   // items of the current chunk handed out
+    int state = LS_DONE;
+    uint32_t q = 0, slot = 0;                              // this lane's path | launch << 8, and pixel slot
+    Ray ray;
+    PathState ps;
+    HitRec hr;
+    Trav tr;
+    auto start = [&](uint32_t sub, uint32_t path, uint32_t lc, uint32_t px, uint32_t rec) {
+        if (sub == ~0u) { state = LS_DONE; return; }       // render's per-sample prologue (:817-844)
+        q = path | (lc << 8);
+        slot = sub * 64u + px;
+        uint32_t x, y;
+        sub_pixel(p, sub, px, x, y);
+        uint32_t s1 = x * seed[rec][0];                    // x * (first frame + frame)
+        uint32_t s2 = y * seed[rec][1];
+        if (path & 1u) (void)hash_seeds(s1, s2);           // the frame's second sample
+        path_begin(ps, s1, s2);
+        const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
+        hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
+        hr.bv = b.x;
+        if constexpr (prim_has_dir<FEAT>()) {
+            hr.su = hr.sv = 0.f;
+            ray.o = p.cam_o;
+            ray.d = mk4(b.y, b.z, b.w, (p.cam_d.w + p.cx.w) + p.cy.w);   // camera_ray's .w
+        } else {
+            hr.su = b.y; hr.sv = b.z;
+            ray = camera_ray(p, x, y);
+        }
+        state = LS_SHADE;
+    };
+    // every lane idle (the wave's first chunk too): the next chunk, waiting
+    // for the ring if need be; false: the session is over for this wave
+    auto wait_chunk = [&]() -> bool {
+        const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            ring = grab(cur_sub, cur_q, cur_L, cslot);
+            if (ring != WAIT) return ring == GOT;
+            // failsafe: a wave that waited twice the session's idle limit
+            // leaves (the ring wave retires the session after one)
+            if ((uint32_t)__builtin_amdgcn_s_memrealtime() - t0 > 2u * p.svc_idle_ticks + 200000u) return false;
+            __builtin_amdgcn_s_sleep(32);
+        }
+    };
+    if (!wait_chunk()) return;
+    next = 64u;
+    start(cur_sub, cur_q, cur_L, (uint32_t)lane, cslot);
+    for (;;) {
+        if (state == LS_SETUP) {
+            if (intersect_spheres<false, FEAT>(p, ray, hr, cnt)) {
+                trav_init<FEAT>(p, ray, hr.t, tr, L);
+                state = LS_TRAV;
+            } else {
+                state = LS_SHADE;
+            }
+        }
+        if (HAS(F_MESH)) {
+            for (;;) {
+                const int n_trav = __popcll(__ballot(state == LS_TRAV));
+                if (n_trav == 0) break;
+                const int n_shade = __popcll(__ballot(state == LS_SHADE));
+                if (n_shade >= VR_SHADE_BATCH && n_shade * VR_SHADE_RATIO >= n_trav) break;
+                if (cur_sub == ~0u && n_shade > 0 && n_shade * VR_DRAIN_SHADE_NUM >= n_trav * VR_DRAIN_SHADE_DEN) break;
+                if (state == LS_TRAV) {
+                    trav_iter<STACK, false, FEAT>(p, ray, tr, L, cnt);
+                    if (tr.nodeAddr == kSentinel) {
+                        trav_finish(tr, hr);
+                        state = LS_SHADE;
+                    }
+                }
+            }
+        }
+        bool ended = false;
+        if (state == LS_SHADE) {
+            vr4 out;
+            if (bounce_step<false, FEAT>(p, ray, hr, ps, out, cnt)) {
+                svc_store_path(p, q >> 8, q & 0xffu, slot, out, ps.depth);
+                ended = true;
+            } else {
+                state = LS_SETUP;
+            }
+        }
+        const unsigned long long em = __ballot(ended);
+        if (em != 0ull) {
+            const uint32_t need = (uint32_t)__popcll(em);
+            uint32_t nsub = ~0u, nq = 0, nL = 0;
+            if (next + need > 64u && cur_sub != ~0u) {
+                ring = grab(nsub, nq, nL, cslot ^ 1u);
+                if (ring != GOT) nsub = ~0u;
+            }
+            if (ended) {
+                const uint32_t r = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                if (r < 64u) start(cur_sub, cur_q, cur_L, r, cslot);
+                else start(nsub, nq, nL, r - 64u, cslot ^ 1u);
+            }
+            if (next + need > 64u) { cur_sub = nsub; cur_q = nq; cur_L = nL; cslot ^= 1u; next = next + need - 64u; }
+            else next += need;
+        }
+        if (__ballot(state != LS_DONE) == 0ull) {
+            if (ring == DONE || !wait_chunk()) break;
+            next = 64u;
+            start(cur_sub, cur_q, cur_L, (uint32_t)lane, cslot);
+        }
+    }
+}
+
+// residency of the service kernel (waves per SIMD; 0: the scene kernel's)
+#ifndef VR_SVC_WAVES
+#define VR_SVC_WAVES 0
+#endif
+constexpr int svc_waves(int stack, bool c) { return VR_SVC_WAVES > 0 && stack <= 24 ? VR_SVC_WAVES : path_waves(stack, c); }
+constexpr int svc_cache_nodes(int stack, int bt, bool c) {
+    return (163840 / (4 * svc_waves(stack, c) * 64 / bt) - bt - stack * bt * 4) / 56 > 0
+               ? (163840 / (4 * svc_waves(stack, c) * 64 / bt) - bt - stack * bt * 4) / 56 : 1;
+}
+template <int STACK, uint32_t FEAT, int BT>
+__global__ void __launch_bounds__(BT, svc_waves(STACK, cornell_kernel<FEAT>())) render_service_kernel(const RenderParams p)
+{
+    constexpr int CN = svc_cache_nodes(STACK, BT, cornell_kernel<FEAT>());
+    __shared__ int lds_stack[STACK * BT];
+    __shared__ vr4 lds_nodes[3 * CN];
+    __shared__ int2 lds_idx[CN];
+    const Lds L = lds_setup<FEAT, BT>(p, lds_stack, lds_nodes, lds_idx, CN, (int)threadIdx.x);
+    service_body<STACK, FEAT, BT>(p, L);
+}
+
 // ---- host launchers --------------------------------------------------------
 // Feature specialisations, smallest first (BASELINE configs C1..C5); the
 // generic kernel covers everything else, deep trees and the counting variant.
@@ -1713,14 +2007,36 @@ inline void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
 // One scene specialisation, production (FEAT) or instrumented
 // (FEAT | F_COUNT_EXEC: same launch shape, residency, node-loop threshold and
 // queues as the production kernel of the same scene, plus load counters).
+// The render service's persistent kernel (one per session): 256-thread
+// blocks at the scene kernel's residency, one resident set.
+template <int STACK, uint32_t FEAT>
+inline void launch_service_wave(const RenderParams& p, hipStream_t s)
+{
+    constexpr uint32_t F = FEAT | F_SERVICE;
+    constexpr bool C = cornell_kernel<F>();
+    constexpr int BT = kBlockThreads;
+    // the session's camera-ray hits (camera, scene and tiling are fixed for it)
+    hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(p.path_stride / kBlockThreads), dim3(kBlockThreads), 0, s, p);
+    const uint32_t per_cu = (uint32_t)(4 * svc_waves(STACK, C) * 64 / BT);
+    hipLaunchKernelGGL((render_service_kernel<STACK, F, BT>), dim3(p.wave_blocks * per_cu), dim3(BT), 0, s, p);
+}
+
 template <uint32_t FEAT>
-inline void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s)
+inline void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool svc = false)
 {
     constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;
     if constexpr ((FEAT & F_MESH) == 0u) {
         // sphere-only scenes: one pixel per thread, primary hit shared by its paths
         hipLaunchKernelGGL((render_kernel<16, CNT, FEAT>), dim3(n_tiles * p.split), dim3(kBlockThreads), 0, s, p);
-    } else {
+    } else if constexpr (!CNT) {
+        if (svc) {                                  // a render-service session (mesh scenes only)
+            if (stack_depth <= 16) launch_service_wave<16, FEAT>(p, s);
+            else if (stack_depth <= 24) launch_service_wave<24, FEAT>(p, s);
+            else launch_service_wave<32, FEAT>(p, s);
+            return;
+        }
+    }
+    if constexpr ((FEAT & F_MESH) != 0u) {
         // mesh scenes: the path-pool kernel (traversal divergence)
         if ((p.flags & F_MESH) == 0u)
             hipLaunchKernelGGL((render_kernel<16, CNT, FEAT>), dim3(n_tiles * p.split), dim3(kBlockThreads), 0, s, p);
@@ -1734,13 +2050,14 @@ inline void launch_spec(const RenderParams& p, uint32_t n_tiles, int stack_depth
 }
 
 // Per-specialisation launchers, one translation unit each (vr_spec_*.hip);
-// exec = the instrumented copy (F_COUNT_EXEC).
-void launch_spec_c1(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
-void launch_spec_c2(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
-void launch_spec_c3(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
-void launch_spec_c4(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
-void launch_spec_c5(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
-void launch_spec_generic(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec);
+// mode 0 production, 1 the instrumented copy (F_COUNT_EXEC), 2 the render
+// service's persistent kernel (mesh scenes).
+void launch_spec_c1(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
+void launch_spec_c2(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
+void launch_spec_c3(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
+void launch_spec_c4(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
+void launch_spec_c5(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
+void launch_spec_generic(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
 // trees deeper than 30 levels (64-entry stacks), production or instrumented
 void launch_spec_deep(const RenderParams& p, uint32_t n_tiles, hipStream_t s, bool exec);
 // the reference algorithm's counting variant (strict traversal, in place)

@@ -37,6 +37,10 @@ enum Flags : uint32_t {
     // order and lets idle lanes help the last traversals (vr_kernel.hip);
     // a separate instantiation, so the whole-frame kernels keep those registers
     F_SMALL = 1u << 14,
+    // compile-time only: the render service's persistent kernel (render_service_kernel):
+    // consecutive launches of a session from a descriptor ring, tagged
+    // primary records, results per launch slot (vrhip_api.cpp Session)
+    F_SERVICE = 1u << 15,
 };
 constexpr int kMaxFramesPerLaunch = 64;
 
@@ -76,6 +80,45 @@ static_assert((VR_QUEUES_LARGE & (VR_QUEUES_LARGE - 1)) == 0 && VR_QUEUES_LARGE 
 static_assert((VR_QUEUES_HDRI & (VR_QUEUES_HDRI - 1)) == 0 && VR_QUEUES_HDRI % 8 == 0,
               "VR_QUEUES_HDRI: power of two, multiple of 8");
 constexpr uint32_t kQueueStride = 256;
+
+// ---- render service (vrhip_set_service; vr_kernel.hpp service_body) --------
+// A session is a run of render launches on one persistent kernel: the host
+// appends launch descriptors to a ring in host-pinned memory and bumps
+// `posted`; a polling wave mirrors them into device memory; every wave takes
+// chunks of launch L, then L + 1, ... so the launches' drains overlap.
+constexpr uint32_t kSvcMaxLaunches = 32;          // launch slots per session
+struct SvcLaunch {                                 // one launch of a session (272 B)
+    uint32_t first_frame, n_frames, pad0, pad1;
+    uint32_t times[kMaxFramesPerLaunch];
+};
+constexpr uint32_t kSvcLaunchWords = (uint32_t)(sizeof(SvcLaunch) / 4);
+struct SvcHostCtl {                                // host-pinned (coherent), written by the host only
+    uint32_t posted;                               // launches posted: desc[0, posted) are valid
+    uint32_t closed;                               // 1: no launch follows `posted` (written after it)
+    uint32_t pad[30];
+    SvcLaunch desc[kSvcMaxLaunches];
+};
+constexpr uint32_t kSvcClosed = 0x80000000u;
+struct SvcDevCtl {                                 // device memory, zeroed when a session opens
+    uint32_t ctl;                                  // mirror of the host ring: posted | closed (kSvcClosed), only grows
+    uint32_t pad0[31];
+    uint32_t pad1[32];
+    SvcLaunch desc[kSvcMaxLaunches];               // device copies of the descriptors (sc1 stores, then ctl)
+};
+// per launch: work-queue heads and drained-queue mask, kQueueStride words apart
+constexpr uint32_t kSvcQctlWords = (VR_MAX_QUEUES + 1u) * kQueueStride;
+// the session finish pass (svc_finish_kernel): per launch, its frame count
+// and which images (bit 0 RGBA8, 1 accum, 2 depth: vrhip_comm_gather's
+// `what`) to stage for a deferred gather
+struct SvcFinish {
+    uint32_t n;                                    // launches in the session
+    uint32_t first_frame;                          // frame number of launch 0's first frame
+    uint32_t n_frames[kSvcMaxLaunches];
+    uint32_t gather[kSvcMaxLaunches];
+    uint8_t* staging;                              // per launch: stage_bytes (owned pixels x 24 B: rgba, depth, accum)
+    size_t stage_bytes;
+    uint32_t stage_pixels;                         // pixels per staged image (the most any rank owns)
+};
 
 struct RenderParams {
     vr4 cam_o, cam_d, cx, cy;        // cx, cy precomputed exactly as PathTracer.cu:833-836
@@ -132,6 +175,13 @@ struct RenderParams {
     u8x4* rgba;
     u8x4* depth;
     unsigned long long* counters;    // kCounters entries (counting variant only)
+    // render service launches (F_SERVICE) only
+    SvcHostCtl* svc_host;            // device pointer of the host-pinned descriptor ring
+    SvcDevCtl* svc_dev;
+    uint32_t* svc_qctl;              // kSvcQctlWords per launch slot
+    size_t svc_slot_bytes;           // result scratch per launch slot: 2 svc_kmax rows of path_stride vr3, then path_w
+    uint32_t svc_kmax;               // frames per launch a slot holds
+    uint32_t svc_idle_ticks;         // 100 MHz ticks with no new launch after which the service retires
     uint32_t times[kMaxFramesPerLaunch];
 };
 
@@ -141,6 +191,10 @@ struct RenderParams {
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int count, void* stream);
 // use_scratch launches: sums the per-path results of launch_render in path order
 int launch_finish(const RenderParams& p, uint32_t n_tiles, void* stream);
+// render service: the persistent kernel of a session (mesh scenes), and the
+// session's finish pass (sums every launch's results in path order)
+int launch_service(const RenderParams& p, uint32_t n_tiles, int stack_depth, void* stream);
+int launch_service_finish(const RenderParams& p, const SvcFinish& f, uint32_t n_tiles, void* stream);
 // sorts the sub-tiles of each XCD by the costs a launch measured (for the next launch on the same scratch)
 int launch_order(uint32_t* cost, uint32_t* order, uint32_t n_sub, uint32_t cap, void* stream);
 int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);

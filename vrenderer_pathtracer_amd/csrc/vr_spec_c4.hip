@@ -5,10 +5,10 @@
 
 namespace vr {
 
-void launch_spec_c4(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec)
+void launch_spec_c4(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode)
 {
-    if (exec) launch_spec<kFeatHdriBrdfSphere | F_EXACT | F_COUNT_EXEC>(p, n_tiles, stack_depth, s);
-    else launch_spec<kFeatHdriBrdfSphere | F_EXACT>(p, n_tiles, stack_depth, s);
+    if (mode == 1) launch_spec<kFeatHdriBrdfSphere | F_EXACT | F_COUNT_EXEC>(p, n_tiles, stack_depth, s);
+    else launch_spec<kFeatHdriBrdfSphere | F_EXACT>(p, n_tiles, stack_depth, s, mode == 2);
 }
 
 } // namespace vr

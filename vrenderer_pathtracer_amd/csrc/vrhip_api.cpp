@@ -11,6 +11,7 @@
 #include <hip/hip_gl_interop.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -128,7 +129,8 @@ struct vrhip_ctx {
     // render-kernel start/stop event pairs not yet added to the totals (read
     // without blocking at the next render, all of them by vrhip_kernel_stats),
     // and recycled events
-    std::deque<std::pair<hipEvent_t, hipEvent_t>> kev_pending;
+    struct Span { hipEvent_t first, second; uint32_t launches; };
+    std::deque<Span> kev_pending;
     std::vector<hipEvent_t> kev_free;
     bool timed = false;          // ev0/ev1 hold the last render
     double kernel_ms_total = 0.0;    // union of the launches' render-kernel spans (overlapping launches count once)
@@ -142,6 +144,42 @@ struct vrhip_ctx {
     unsigned long long* counters = nullptr;
     // GL interop (colour, depth textures registered by the display host)
     hipGraphicsResource_t gl_res[2] = { nullptr, nullptr };
+    // render service (vrhip_set_service): a session of launches on one
+    // persistent kernel (vr_kernel.hpp service_body), see svc_open
+    struct Session {
+        bool open = false;
+        hipStream_t s = nullptr;                  // the service stream
+        // descriptor rings in host-pinned coherent memory, one per session in
+        // turn: a closed session's kernel may still read its ring while the
+        // next session fills the other (ring_done: after that kernel)
+        vr::SvcHostCtl* rings[2] = { nullptr, nullptr };
+        vr::SvcHostCtl* rings_dev[2] = { nullptr, nullptr };
+        hipEvent_t ring_done[2] = { nullptr, nullptr };
+        bool ring_used[2] = { false, false };
+        uint32_t ring_i = 0;
+        vr::SvcHostCtl* host = nullptr;           // the open session's ring
+        vr::SvcDevCtl* dev = nullptr;             // device mirror of the ring
+        uint32_t* qctl = nullptr; size_t qctl_slots = 0;    // work-queue heads per launch slot
+        uint8_t* scratch = nullptr; size_t scratch_cap = 0; // launch slots' path results
+        vr4* prim = nullptr; size_t prim_cap = 0;           // the session's primary records, 2 float4 per owned pixel
+        uint8_t* staging = nullptr; size_t staging_cap = 0; // deferred gathers: per launch slot
+        uint32_t slots = 0, kmax = 0, posted = 0;
+        size_t slot_bytes = 0;
+        int stack = 16;
+        uint32_t n_tiles = 0;
+        vr::RenderParams p{};                     // the session's launch parameters
+        vr::RenderParams key{};                   // what must not change within a session (svc_key)
+        vr::SvcFinish fin{};
+        std::vector<std::pair<uint32_t, int>> gathers;   // deferred vrhip_comm_gather: (launch, what)
+        std::chrono::steady_clock::time_point last_post;
+        hipEvent_t k0 = nullptr, k1 = nullptr;    // the service kernel's span
+        hipEvent_t finished = nullptr;            // recorded on `stream` after the session's finish pass
+        bool finished_used = false;
+    } svc;
+    int service = -1;                             // 1 every production mesh launch, 0 never, -1 automatic
+    // multi-device renderer (vrhip_create_multi): the lead context holds every
+    // member context (itself first); settings fan out to all of them
+    std::vector<vrhip_ctx*> group;
     // multi-GPU tile gather (vrhip_comm_*): one RCCL communicator per context
     ncclComm_t comm = nullptr;
     uint8_t* comm_send = nullptr;    // this rank's packed tiles (largest element, 16 B/pixel)
@@ -149,6 +187,11 @@ struct vrhip_ctx {
     size_t comm_slot = 0;            // bytes per rank slot (max owned pixels x 16 B)
     uint32_t comm_rank = 0, comm_n = 0;   // the communicator's rank and size (tiling fixed while it exists)
 };
+
+static void svc_free(vrhip_ctx* c);
+static int svc_close(vrhip_ctx* c);
+static int refuse_multi(vrhip_ctx* c, const char* what);
+static int multi_gather(vrhip_ctx* c, int what);
 
 namespace {
 
@@ -164,6 +207,8 @@ int set_device(vrhip_ctx* c) { HIP_TRY(hipSetDevice(c->device)); return VRHIP_OK
 
 int clear_accum(vrhip_ctx* c)
 {
+    int rc = svc_close(c);                        // the open session's results come first
+    if (rc != VRHIP_OK) return rc;
     c->frame = 1;
     HIP_TRY(hipMemsetAsync(c->accum, 0, sizeof(vr4) * (size_t)c->W * c->H, c->stream));
     return VRHIP_OK;
@@ -432,6 +477,8 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
 // Every call that replaces device buffers or the stream goes through here.
 void quiesce(vrhip_ctx* c)
 {
+    (void)svc_close(c);
+    if (c->svc.s) (void)hipStreamSynchronize(c->svc.s);
     for (auto& l : c->lane)
         if (l.s) (void)hipStreamSynchronize(l.s);
     c->join = true;
@@ -477,6 +524,7 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     c->W = width; c->H = height;
     c->fov_scale = default_fov_scale();
     if (const char* e = std::getenv("VRHIP_COST_ORDER")) c->cost_order = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VRHIP_SERVICE")) c->service = std::max(-1, std::min(1, std::atoi(e)));
     int rc;
     if ((rc = set_device(c)) != VRHIP_OK) { delete c; return rc; }
     auto cleanup = [&](int code) { vrhip_destroy(c); return code; };
@@ -526,7 +574,14 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
 int vrhip_destroy(vrhip_ctx* c)
 {
     if (!c) return VRHIP_OK;
+    if (!c->group.empty()) {                          // a multi-device context: every member, the lead last
+        std::vector<vrhip_ctx*> ms;
+        ms.swap(c->group);
+        for (vrhip_ctx* m : ms) { (void)hipSetDevice(m->device); (void)svc_close(m); if (m->stream) (void)hipStreamSynchronize(m->stream); }
+        for (size_t i = ms.size(); i-- > 1;) vrhip_destroy(ms[i]);
+    }
     (void)hipSetDevice(c->device);
+    (void)svc_close(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     quiesce(c);
     dfree(c->accum); dfree(c->rgba); dfree(c->depth); dfree(c->cam_sxy);
@@ -548,6 +603,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (auto& pr : c->kev_pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    svc_free(c);
     for (hipEvent_t e : c->kev_free) (void)hipEventDestroy(e);
     if (c->kev_origin) (void)hipEventDestroy(c->kev_origin);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -557,9 +613,13 @@ int vrhip_destroy(vrhip_ctx* c)
 
 int vrhip_set_stream(vrhip_ctx* c, void* s)
 {
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_set_stream");
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     // work queued on the old stream (finish passes) must not reorder with the new one
-    if (c->stream && hipSetDevice(c->device) == hipSuccess) (void)hipStreamSynchronize(c->stream);
+    if (c->stream && hipSetDevice(c->device) == hipSuccess) {
+        (void)svc_close(c);
+        (void)hipStreamSynchronize(c->stream);
+    }
     quiesce(c);
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return VRHIP_OK;
@@ -567,7 +627,7 @@ int vrhip_set_stream(vrhip_ctx* c, void* s)
 
 void* vrhip_get_stream(vrhip_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-int vrhip_set_camera(vrhip_ctx* c, const float origin[3], const float dir[3], const float up[3],
+static int one_set_camera(vrhip_ctx* c, const float origin[3], const float dir[3], const float up[3],
                      const float right[3], float fov_scale)
 {
     if (!c || !origin || !dir || !up || !right) return fail(VRHIP_ERR_INVALID, "bad camera arguments");
@@ -578,26 +638,26 @@ int vrhip_set_camera(vrhip_ctx* c, const float origin[3], const float dir[3], co
     return clear_accum(c);
 }
 
-int vrhip_clear(vrhip_ctx* c)
+static int one_clear(vrhip_ctx* c)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     int rc = set_device(c); if (rc) return rc;
     return clear_accum(c);
 }
 
-int vrhip_set_fresnel(vrhip_ctx* c, float coef, float power)
+static int one_set_fresnel(vrhip_ctx* c, float coef, float power)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     c->fresnel_coef = coef; c->fresnel_pow = power;
     return VRHIP_OK;
 }
 
-int vrhip_use_cornell_box(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->cornell = e != 0; return VRHIP_OK; }
-int vrhip_use_example_sphere(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->example = e != 0; return VRHIP_OK; }
-int vrhip_set_strict_traversal(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->strict = e != 0; return VRHIP_OK; }
-int vrhip_use_brdf(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->view_brdf = e != 0; return VRHIP_OK; }
+static int one_use_cornell_box(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->cornell = e != 0; return VRHIP_OK; }
+static int one_use_example_sphere(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->example = e != 0; return VRHIP_OK; }
+static int one_set_strict_traversal(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->strict = e != 0; return VRHIP_OK; }
+static int one_use_brdf(vrhip_ctx* c, int e) { if (!c) return fail(VRHIP_ERR_INVALID, "null ctx"); c->view_brdf = e != 0; return VRHIP_OK; }
 
-int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, const float* verts,
+static int one_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, const float* verts,
                            const float* normals, const float* tangents, const float* uvs, size_t n_slots)
 {
     if (!c || !bvh || !verts || !normals || !tangents || !uvs) return fail(VRHIP_ERR_INVALID, "null mesh array");
@@ -642,7 +702,7 @@ int vrhip_upload_mesh_indexed(vrhip_ctx* c, const float* positions, const float*
                                   (const float*)m.uvs.data(), m.verts.size());
 }
 
-int vrhip_upload_hdr(vrhip_ctx* c, const float* rgba, uint32_t w, uint32_t h)
+static int one_upload_hdr(vrhip_ctx* c, const float* rgba, uint32_t w, uint32_t h)
 {
     if (!c || !rgba || w == 0 || h == 0) return fail(VRHIP_ERR_INVALID, "bad hdr arguments");
     int rc = set_device(c); if (rc) return rc;
@@ -652,7 +712,7 @@ int vrhip_upload_hdr(vrhip_ctx* c, const float* rgba, uint32_t w, uint32_t h)
     return VRHIP_OK;
 }
 
-int vrhip_upload_hdr_half(vrhip_ctx* c, const uint16_t* rgba_half, uint32_t w, uint32_t h)
+static int one_upload_hdr_half(vrhip_ctx* c, const uint16_t* rgba_half, uint32_t w, uint32_t h)
 {
     if (!c || !rgba_half || w == 0 || h == 0) return fail(VRHIP_ERR_INVALID, "bad hdr arguments");
     int rc = set_device(c); if (rc) return rc;
@@ -670,7 +730,7 @@ int vrhip_upload_hdr_half(vrhip_ctx* c, const uint16_t* rgba_half, uint32_t w, u
     return VRHIP_OK;
 }
 
-int vrhip_upload_texture(vrhip_ctx* c, int type, const float* rgba, uint32_t w, uint32_t h)
+static int one_upload_texture(vrhip_ctx* c, int type, const float* rgba, uint32_t w, uint32_t h)
 {
     if (!c || !rgba || w == 0 || h == 0 || type < 0 || type > 2) return fail(VRHIP_ERR_INVALID, "bad texture arguments");
     int rc = set_device(c); if (rc) return rc;
@@ -680,7 +740,7 @@ int vrhip_upload_texture(vrhip_ctx* c, int type, const float* rgba, uint32_t w, 
     return VRHIP_OK;
 }
 
-int vrhip_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
+static int one_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
 {
     const size_t n = 90u * 90u * 360u / 2u;    // BRDF_SAMPLING_RES_* (include/vRenderer.h:23-25)
     if (!c || !table || n_floats != 3 * n) return fail(VRHIP_ERR_INVALID, "BRDF table must hold 3*1458000 floats");
@@ -741,6 +801,7 @@ int vrhip_gl_present(vrhip_ctx* c)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     const void* src[2] = { c->rgba, c->depth };
     for (int i = 0; i < 2; ++i) {
         if (!c->gl_res[i]) continue;
@@ -806,7 +867,7 @@ static int account_pending(vrhip_ctx* c, bool wait)
             std::sort(out.begin(), out.end());
             u.swap(out);
         }
-        c->launches_total += 1;
+        c->launches_total += pr.launches;
         c->kev_pending.pop_front();
         if (!keep_start) c->kev_free.push_back(pr.first);
         c->kev_free.push_back(pr.second);
@@ -895,6 +956,214 @@ static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t p
     return VRHIP_OK;
 }
 
+
+// ---- render service sessions ------------------------------------------------
+// Back-to-back render calls on mesh scenes (vrhip_set_service: automatically
+// behind a launch still in flight for the launches that overlap on the path
+// streams -- shards and small frames -- or always) post their launches to
+// ONE persistent kernel (vr_kernel.hpp service_body) through a descriptor
+// ring in host-pinned memory, so a launch's drain overlaps the next launch's
+// paths.  Each launch writes its paths' results to its own scratch slot; when
+// the session closes -- at the next call that is not a render (sync, read-back,
+// upload, any setting or buffer access: svc_close), when its slots are full,
+// or when a launch does not fit the session -- one finish pass sums every
+// pixel's paths launch by launch in path order, stages the images of
+// launches whose gather was deferred (vrhip_comm_gather inside a session),
+// and the gathers run.  Results are bit-identical to launch-by-launch
+// rendering; only their time of arrival changes.
+#ifndef VR_SVC_IDLE_MS
+#define VR_SVC_IDLE_MS 20            // the kernel retires after this long without a new launch
+#endif
+#ifndef VR_SVC_POST_MS
+#define VR_SVC_POST_MS 5             // the host posts to a session only within this of its last post
+#endif
+
+static void svc_free(vrhip_ctx* c)
+{
+    auto& S = c->svc;
+    if (S.s) (void)hipStreamSynchronize(S.s);
+    for (int i = 0; i < 2; ++i) {
+        if (S.rings[i]) (void)hipHostFree(S.rings[i]);
+        if (S.ring_done[i]) (void)hipEventDestroy(S.ring_done[i]);
+        S.rings[i] = S.rings_dev[i] = nullptr;
+        S.ring_done[i] = nullptr;
+        S.ring_used[i] = false;
+    }
+    S.host = nullptr;
+    dfree(S.dev); dfree(S.qctl); dfree(S.scratch); dfree(S.prim); dfree(S.staging);
+    S.qctl_slots = S.scratch_cap = S.prim_cap = S.staging_cap = 0;
+    if (S.k0) (void)hipEventDestroy(S.k0);
+    if (S.k1) (void)hipEventDestroy(S.k1);
+    if (S.finished) (void)hipEventDestroy(S.finished);
+    if (S.s) (void)hipStreamDestroy(S.s);
+    S.k0 = S.k1 = S.finished = nullptr;
+    S.s = nullptr;
+    S.open = false;
+}
+
+// The launch parameters that must stay fixed within a session (scene,
+// camera, flags, tiling, frame buffers): per-launch fields cleared.
+static vr::RenderParams svc_key(const vr::RenderParams& p)
+{
+    vr::RenderParams k = p;
+    k.first_frame = k.n_frames = 0;
+    std::memset(k.times, 0, sizeof(k.times));
+    k.split = k.use_scratch = k.small_blocks = k.inline_prim = 0;
+    k.paths = nullptr; k.path_w = nullptr; k.prim = nullptr; k.chunk_ctr = nullptr;
+    k.path_cost = nullptr; k.sub_cost = nullptr; k.sub_order = nullptr; k.order_cap = 0;
+    k.counters = nullptr; k.n_queues = 0;
+    return k;
+}
+
+// Closes the open session: the kernel retires once the ring is drained, then
+// the finish pass and the deferred gathers run on `stream`.  Asynchronous.
+static int svc_close(vrhip_ctx* c)
+{
+    auto& S = c->svc;
+    if (!S.open) return VRHIP_OK;
+    S.open = false;
+    __atomic_store_n(&S.host->closed, 1u, __ATOMIC_RELEASE);
+    HIP_TRY(hipStreamWaitEvent(c->stream, S.k1, 0));
+    S.fin.n = S.posted;
+    const int e = vr::launch_service_finish(S.p, S.fin, S.n_tiles, c->stream);
+    if (e != 0) return fail(VRHIP_ERR_HIP, std::string("service finish launch: ") + hipGetErrorString((hipError_t)e));
+    // deferred gathers, in call order; rank 0 keeps its own tiles from the
+    // finish pass (the final state) and unpacks the other ranks' of every gather
+    for (const auto& g : S.gathers) {
+        const int what = g.second;
+        const size_t esz = what == 1 ? 16u : 4u;
+        const size_t off = what == 0 ? 0u : what == 2 ? 4u * (size_t)S.fin.stage_pixels : 8u * (size_t)S.fin.stage_pixels;
+        const uint8_t* send = S.staging + (size_t)g.first * S.fin.stage_bytes + off;
+        const size_t bytes = (size_t)S.fin.stage_pixels * esz;
+        const ncclResult_t r = ncclGather(send, c->comm_recv, bytes, ncclUint8, 0, c->comm, c->stream);
+        if (r != ncclSuccess) return fail(VRHIP_ERR_COMM, std::string("ncclGather: ") + ncclGetErrorString(r));
+        if (c->rank == 0) {
+            void* dst = what == 1 ? (void*)c->accum : what == 2 ? (void*)c->depth : (void*)c->rgba;
+            for (uint32_t rr = 1; rr < c->nranks; ++rr) {
+                const uint32_t n_owned = owned_tiles_of(c->W, c->H, rr, c->nranks);
+                const int ee = vr::launch_pack_tiles(c->comm_recv + (size_t)rr * bytes, dst, (uint32_t)esz, c->W,
+                                                     c->W / 16u, n_owned, rr, c->nranks, 1, c->stream);
+                if (ee) return fail(VRHIP_ERR_HIP, "unpack launch failed");
+            }
+        }
+    }
+    S.gathers.clear();
+    HIP_TRY(hipEventRecord(S.finished, c->stream));
+    S.finished_used = true;
+    // the session's kernel span: one span covering all its launches
+    hipEvent_t a = nullptr, b = nullptr;
+    if ((a = S.k0) && (b = S.k1)) {
+        S.k0 = S.k1 = nullptr;
+        c->kev_pending.push_back({ a, b, S.posted });
+    }
+    return VRHIP_OK;
+}
+
+// Opens a session for launches of up to kmax frames with parameters p.
+static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t n_tiles, uint32_t kmax)
+{
+    auto& S = c->svc;
+    if (!S.s) {
+        HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&S.finished, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i) {
+            HIP_TRY(hipHostMalloc((void**)&S.rings[i], sizeof(vr::SvcHostCtl), hipHostMallocCoherent | hipHostMallocMapped));
+            HIP_TRY(hipHostGetDevicePointer((void**)&S.rings_dev[i], S.rings[i], 0));
+            HIP_TRY(hipEventCreateWithFlags(&S.ring_done[i], hipEventDisableTiming));
+        }
+        HIP_TRY(hipMalloc((void**)&S.dev, sizeof(vr::SvcDevCtl)));
+    }
+    // this session's ring: the other one's kernel may still run; this one's
+    // kernel (two sessions back) must have retired before the host rewrites it
+    const uint32_t ri = S.ring_i;
+    S.ring_i ^= 1u;
+    if (S.ring_used[ri]) HIP_TRY(hipEventSynchronize(S.ring_done[ri]));
+    const size_t stride = p.path_stride;
+    const size_t slot_bytes = ((12u * 2u * (size_t)kmax * stride + 4u * stride) + 255u) & ~(size_t)255u;
+    static const size_t budget = [] {
+        const char* e = std::getenv("VRHIP_SERVICE_BYTES");
+        return e ? (size_t)std::atoll(e) : ((size_t)8 << 30);
+    }();
+    const uint32_t slots = (uint32_t)std::min<size_t>(vr::kSvcMaxLaunches, budget / slot_bytes);
+    if (slots < 2) return fail(VRHIP_ERR_NOMEM, "render service: the budget holds fewer than 2 launch slots");
+    const uint32_t stage_px = owned_tiles_of(c->W, c->H, 0, c->nranks) * 256u;   // rank 0 owns the most tiles
+    const size_t stage_bytes = (24u * (size_t)stage_px + 255u) & ~(size_t)255u;
+    auto grow = [&](auto*& ptr, size_t& cap, size_t need) -> int {
+        if (need <= cap) return VRHIP_OK;
+        // the previous session's kernel and finish pass may still use the old buffer
+        if (S.s) HIP_TRY(hipStreamSynchronize(S.s));
+        if (S.finished_used) HIP_TRY(hipEventSynchronize(S.finished));
+        dfree(ptr);
+        cap = 0;
+        HIP_TRY(hipMalloc((void**)&ptr, need));
+        cap = need;
+        return VRHIP_OK;
+    };
+    int rc;
+    if ((rc = grow(S.scratch, S.scratch_cap, (size_t)slots * slot_bytes)) != VRHIP_OK) return rc;
+    if ((rc = grow(S.prim, S.prim_cap, 32u * stride)) != VRHIP_OK) return rc;
+    if ((rc = grow(S.staging, S.staging_cap, (size_t)slots * stage_bytes)) != VRHIP_OK) return rc;
+    if ((rc = grow(S.qctl, S.qctl_slots, (size_t)slots * vr::kSvcQctlWords * 4u)) != VRHIP_OK) return rc;
+    if (!S.k0 && (rc = take_event(c, &S.k0)) != VRHIP_OK) return rc;
+    if (!S.k1 && (rc = take_event(c, &S.k1)) != VRHIP_OK) return rc;
+    S.slot_bytes = slot_bytes; S.slots = slots; S.kmax = kmax; S.posted = 0;
+    S.stack = stack; S.n_tiles = n_tiles;
+    S.p = p;
+    S.p.paths = reinterpret_cast<vr3*>(S.scratch);
+    S.p.prim = S.prim;
+    S.host = S.rings[ri];
+    S.p.svc_host = S.rings_dev[ri]; S.p.svc_dev = S.dev; S.p.svc_qctl = S.qctl;
+    S.p.svc_slot_bytes = slot_bytes; S.p.svc_kmax = kmax;
+    S.p.svc_idle_ticks = (uint32_t)VR_SVC_IDLE_MS * 100000u;
+    S.key = svc_key(p);
+    std::memset(&S.fin, 0, sizeof(S.fin));
+    S.fin.first_frame = c->frame;
+    S.fin.staging = S.staging; S.fin.stage_bytes = stage_bytes; S.fin.stage_pixels = stage_px;
+    S.gathers.clear();
+    // the ring: nothing posted, open (the kernel launch below orders these
+    // host stores before the kernel's first read)
+    S.host->posted = 0; S.host->closed = 0;
+    // everything queued on `stream` first (uploads, clears, earlier finish passes)
+    HIP_TRY(hipEventRecord(c->ev_join, c->stream));
+    HIP_TRY(hipStreamWaitEvent(S.s, c->ev_join, 0));
+    HIP_TRY(hipMemsetAsync(S.dev, 0, sizeof(vr::SvcDevCtl), S.s));
+    HIP_TRY(hipMemsetAsync(S.qctl, 0, (size_t)slots * vr::kSvcQctlWords * 4u, S.s));
+    HIP_TRY(hipEventRecord(S.k0, S.s));
+    const int e = vr::launch_service(S.p, n_tiles, stack, S.s);
+    if (e != 0) return fail(VRHIP_ERR_HIP, std::string("service launch: ") + hipGetErrorString((hipError_t)e));
+    HIP_TRY(hipEventRecord(S.k1, S.s));
+    HIP_TRY(hipEventRecord(S.ring_done[ri], S.s));
+    S.ring_used[ri] = true;
+    S.open = true;
+    S.last_post = std::chrono::steady_clock::now();
+    return VRHIP_OK;
+}
+
+// Posts one launch of k frames (first frame c->frame) to the open session.
+static void svc_post(vrhip_ctx* c, uint32_t k, const uint32_t* times, uint32_t time_seed)
+{
+    auto& S = c->svc;
+    vr::SvcLaunch& d = S.host->desc[S.posted];
+    d.first_frame = c->frame;
+    d.n_frames = k;
+    for (uint32_t i = 0; i < k; ++i) d.times[i] = times ? times[i] : time_seed;
+    S.fin.n_frames[S.posted] = k;
+    __atomic_store_n(&S.host->posted, S.posted + 1u, __ATOMIC_RELEASE);
+    ++S.posted;
+    S.last_post = std::chrono::steady_clock::now();
+}
+
+// Whether the open session can take a launch of k frames with parameters p.
+static bool svc_fits(const vrhip_ctx* c, const vr::RenderParams& p, uint32_t k)
+{
+    const auto& S = c->svc;
+    if (!S.open || S.posted >= S.slots || k > S.kmax) return false;
+    const auto idle = std::chrono::steady_clock::now() - S.last_post;
+    if (idle > std::chrono::milliseconds(VR_SVC_POST_MS)) return false;
+    const vr::RenderParams key = svc_key(p);
+    return std::memcmp(&key, &S.key, sizeof(key)) == 0;
+}
+
 // count: 0 production, 1 reference-algorithm counting variant (in place, no
 // scratch), 2 instrumented production kernels (same launch shape as 0)
 static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed, int count)
@@ -957,6 +1226,36 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.waves_cap = env_waves;
     const bool wave_kernel = (f & vr::F_MESH) != 0u;   // mesh scenes: the path-pool kernel (scratch + finish pass)
     (void)hipGetLastError();            // launches below report their own errors only
+    // counting launches and anything else than a production mesh launch end a session first
+    {
+        const size_t paths_k = (size_t)p.path_stride * 2u * k_max;
+        const bool ovl_size = paths_k < ((size_t)1 << 24) || (c->nranks > 1 && paths_k < ((size_t)1 << 25));
+        const bool in_flight = c->svc.open || (c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
+        const bool svc = count == 0 && wave_kernel && stack <= 32 && n_tiles > 0 &&
+                         (c->service > 0 || (c->service < 0 && ovl_size && in_flight && c->overlap != 0));
+        if (!svc) {
+            if ((rc = svc_close(c)) != VRHIP_OK) return rc;
+        } else {
+            p.n_queues = c->cornell ? VR_QUEUES : VR_QUEUES_HDRI;
+            static const uint32_t env_q = [] {
+                const char* e = std::getenv("VRHIP_QUEUES");
+                const uint32_t q = e ? (uint32_t)std::atoi(e) : 0u;
+                return (q >= 8 && q <= (uint32_t)VR_MAX_QUEUES && (q & (q - 1)) == 0) ? q : 0u;
+            }();
+            if (env_q) p.n_queues = env_q;
+            uint32_t done = 0;
+            while (done < n_frames) {
+                const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
+                if (c->svc.open && !svc_fits(c, p, k) && (rc = svc_close(c)) != VRHIP_OK) return rc;
+                if (!c->svc.open && (rc = svc_open(c, p, stack, n_tiles, k_max)) != VRHIP_OK) return rc;
+                svc_post(c, k, times ? times + done : nullptr, time_seed);
+                c->frame += k;
+                done += k;
+            }
+            c->last_split = 1; c->last_use_scratch = 1; c->last_kind = 2;
+            return VRHIP_OK;
+        }
+    }
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     uint32_t done = 0;
     while (done < n_frames) {
@@ -1048,7 +1347,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (n_tiles) {
             if ((rc = take_event(c, &k0)) != VRHIP_OK || (rc = take_event(c, &k1)) != VRHIP_OK) return rc;
-            c->kev_pending.emplace_back(k0, k1);
+            c->kev_pending.push_back({ k0, k1, 1u });
             HIP_TRY(hipEventRecord(k0, rs));
         }
         if (count == 0) { c->last_split = p.split; c->last_use_scratch = p.use_scratch; c->last_kind = wave_kernel ? 1u : 0u; }
@@ -1090,7 +1389,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     return VRHIP_OK;
 }
 
-int vrhip_render(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed)
+static int one_render(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed)
 {
     return render_impl(c, n_frames, times, time_seed, 0);
 }
@@ -1098,6 +1397,7 @@ int vrhip_render(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_
 int vrhip_render_counted(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed,
                          uint64_t counters[8])
 {
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_render_counted");
     if (!counters) return fail(VRHIP_ERR_INVALID, "counters is NULL");
     int rc = render_impl(c, n_frames, times, time_seed, 1);
     if (rc) return rc;
@@ -1111,6 +1411,7 @@ int vrhip_render_counted(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times,
 int vrhip_render_profiled(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed,
                           uint64_t counters[VRHIP_PROFILE_COUNTERS])
 {
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_render_profiled");
     if (!counters) return fail(VRHIP_ERR_INVALID, "counters is NULL");
     static_assert(VRHIP_PROFILE_COUNTERS == vr::kCounters + vr::kExecCounters, "profile counter layout");
     int rc = render_impl(c, n_frames, times, time_seed, 2);
@@ -1164,6 +1465,7 @@ int vrhip_debug_counters(vrhip_ctx* c, uint64_t out[16], int reset)
 {
     if (!c || !out) return fail(VRHIP_ERR_INVALID, "null argument");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     if ((rc = ensure_counters(c)) != VRHIP_OK) return rc;
     unsigned long long h[16] = {};
     HIP_TRY(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -1177,6 +1479,7 @@ int vrhip_kernel_stats(vrhip_ctx* c, double* total_ms, uint64_t* launches, int r
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     if ((rc = account_pending(c, true)) != VRHIP_OK) return rc;
     if (total_ms) *total_ms = c->kernel_ms_total;
     if (launches) *launches = c->launches_total;
@@ -1198,10 +1501,11 @@ int vrhip_last_launch_info(vrhip_ctx* c, uint32_t* split, uint32_t* use_scratch,
     return VRHIP_OK;
 }
 
-int vrhip_sync(vrhip_ctx* c)
+static int one_sync(vrhip_ctx* c)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     return VRHIP_OK;
 }
@@ -1217,18 +1521,28 @@ static int readback(vrhip_ctx* c, const void* src, void* dst, size_t bytes)
 {
     if (!c || !dst) return fail(VRHIP_ERR_INVALID, "null argument");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return VRHIP_OK;
 }
 
-int vrhip_read_accum(vrhip_ctx* c, float* out) { return c ? readback(c, c->accum, out, (size_t)c->W * c->H * 16) : fail(VRHIP_ERR_INVALID, "null ctx"); }
+int vrhip_read_accum(vrhip_ctx* c, float* out)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    if (!c->group.empty()) {                          // the accumulation lives on every device: gather it first
+        const int rc = multi_gather(c, 1);
+        if (rc != VRHIP_OK) return rc;
+    }
+    return readback(c, c->accum, out, (size_t)c->W * c->H * 16);
+}
 int vrhip_read_rgba8(vrhip_ctx* c, uint8_t* out) { return c ? readback(c, c->rgba, out, (size_t)c->W * c->H * 4) : fail(VRHIP_ERR_INVALID, "null ctx"); }
 int vrhip_read_depth8(vrhip_ctx* c, uint8_t* out) { return c ? readback(c, c->depth, out, (size_t)c->W * c->H * 4) : fail(VRHIP_ERR_INVALID, "null ctx"); }
 
 int vrhip_device_buffers(vrhip_ctx* c, void** accum, void** rgba8, void** depth8)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    if (set_device(c) == VRHIP_OK) (void)svc_close(c);     // the buffers hold every render so far
     if (accum) *accum = c->accum;
     if (rgba8) *rgba8 = c->rgba;
     if (depth8) *depth8 = c->depth;
@@ -1237,6 +1551,7 @@ int vrhip_device_buffers(vrhip_ctx* c, void** accum, void** rgba8, void** depth8
 
 int vrhip_set_tiling(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks)
 {
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_set_tiling");
     if (!c || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad tiling");
     // the gather buffers and the RCCL communicator are sized for the
     // communicator's tiling: it cannot change while they exist
@@ -1247,14 +1562,23 @@ int vrhip_set_tiling(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks)
     return VRHIP_OK;
 }
 
-int vrhip_set_overlap(vrhip_ctx* c, int mode)
+static int one_set_overlap(vrhip_ctx* c, int mode)
 {
     if (!c || mode < -1 || mode > 1) return fail(VRHIP_ERR_INVALID, "bad overlap mode");
     c->overlap = mode;
     return VRHIP_OK;
 }
 
-int vrhip_set_path_split(vrhip_ctx* c, uint32_t groups)
+static int one_set_service(vrhip_ctx* c, int mode)
+{
+    if (!c || mode < -1 || mode > 1) return fail(VRHIP_ERR_INVALID, "bad service mode");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
+    c->service = mode;
+    return VRHIP_OK;
+}
+
+static int one_set_path_split(vrhip_ctx* c, uint32_t groups)
 {
     if (!c || groups > 2u * vr::kMaxFramesPerLaunch) return fail(VRHIP_ERR_INVALID, "bad path split");
     c->path_split = groups;
@@ -1291,6 +1615,7 @@ int vrhip_pack_tiles(vrhip_ctx* c, int what, void* dst)
 {
     if (!c || !dst || what < 0 || what > 2) return fail(VRHIP_ERR_INVALID, "bad pack arguments");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     int e = vr::launch_pack_tiles(buf_of(c, what), dst, (uint32_t)elem_size(what), c->W, c->W / 16u,
                                   owned_tiles_of(c->W, c->H, c->rank, c->nranks), c->rank, c->nranks, 0, c->stream);
     if (e) return fail(VRHIP_ERR_HIP, "pack launch failed");
@@ -1301,6 +1626,7 @@ int vrhip_unpack_tiles(vrhip_ctx* c, int what, const void* src, uint32_t n_ranks
 {
     if (!c || !src || what < 0 || what > 2 || n_ranks == 0) return fail(VRHIP_ERR_INVALID, "bad unpack arguments");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     const char* s = (const char*)src;
     for (uint32_t r = 0; r < n_ranks; ++r) {
         const uint32_t n_owned = owned_tiles_of(c->W, c->H, r, n_ranks);
@@ -1336,8 +1662,10 @@ int vrhip_comm_unique_id(uint8_t id[VRHIP_COMM_ID_BYTES])
 
 int vrhip_comm_init(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks, const uint8_t id[VRHIP_COMM_ID_BYTES])
 {
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_comm_init");
     if (!c || !id || n_ranks == 0 || rank >= n_ranks) return fail(VRHIP_ERR_INVALID, "bad communicator arguments");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
     dfree(c->comm_send); dfree(c->comm_recv);
     if ((rc = vrhip_set_tiling(c, rank, n_ranks)) != VRHIP_OK) return rc;
@@ -1356,9 +1684,20 @@ int vrhip_comm_init(vrhip_ctx* c, uint32_t rank, uint32_t n_ranks, const uint8_t
 
 int vrhip_comm_gather(vrhip_ctx* c, int what)
 {
+    if (c && !c->group.empty()) {                     // the group's own communicators
+        if (what < 0 || what > 2) return fail(VRHIP_ERR_INVALID, "bad gather arguments");
+        return multi_gather(c, what);
+    }
     if (!c || what < 0 || what > 2) return fail(VRHIP_ERR_INVALID, "bad gather arguments");
     if (!c->comm) return fail(VRHIP_ERR_INVALID, "vrhip_comm_init has not been called");
     int rc = set_device(c); if (rc) return rc;
+    if (c->svc.open && c->svc.posted > 0) {
+        // inside a session: the image after its last launch is staged by the
+        // session's finish pass and gathered when the session closes
+        c->svc.fin.gather[c->svc.posted - 1u] |= 1u << what;
+        c->svc.gathers.emplace_back(c->svc.posted - 1u, what);
+        return VRHIP_OK;
+    }
     // pack -> gather -> (rank 0) unpack, all on the context stream, behind the
     // finish passes that wrote the images
     if (c->rank != c->comm_rank || c->nranks != c->comm_n)
@@ -1374,8 +1713,10 @@ int vrhip_comm_gather(vrhip_ctx* c, int what)
 
 int vrhip_comm_destroy(vrhip_ctx* c)
 {
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_comm_destroy");
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->comm) {
         const ncclResult_t r = ncclCommDestroy(c->comm);
@@ -1389,6 +1730,7 @@ int vrhip_comm_destroy(vrhip_ctx* c)
 int vrhip_last_kernel_ms(vrhip_ctx* c, float* ms)
 {
     if (!c || !ms) return fail(VRHIP_ERR_INVALID, "null argument");
+    if (set_device(c) == VRHIP_OK) (void)svc_close(c);
     if (!c->timed) { *ms = 0.f; return VRHIP_OK; }
     HIP_TRY(hipEventSynchronize(c->ev1));
     HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
@@ -1482,6 +1824,168 @@ int vrhip_validate_flat(const float* bvh, size_t n_bvh_f4, const float* verts, s
     int v = vr::validate_flat(bvh, n_bvh_f4, verts, n_slots, depth, n_nodes);
     if (v != 0) return fail(VRHIP_ERR_BVH, "validation failed (code " + std::to_string(v) + ")");
     return VRHIP_OK;
+}
+
+
+// ---- multi-device renderer (SURVEY 8b create_multi) -------------------------
+// One vrhip_ctx over several GPUs of this process: a member context per
+// device, each owning the 16x16 tiles i, i + n, ... of the image; the RCCL
+// communicators made in one call (ncclCommInitAll); every setting and upload
+// fanned out; vrhip_render renders every device's tiles and gathers the RGBA8
+// and depth tiles to the lead device (one grouped ncclGather each), whose
+// images are then the whole frame (read-back, GL presentation).  The
+// reference's single caller creates one renderer (src/NGLScene.cpp:82-89):
+// through this context it drives all the devices named in VRHIP_DEVICES
+// (integration/vRendererHIP.cpp).
+
+} // extern "C"
+template <typename F>
+static int fanout(vrhip_ctx* c, F&& f)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    if (c->group.empty()) return f(c);
+    for (vrhip_ctx* m : c->group) {
+        const int rc = f(m);
+        if (rc != VRHIP_OK) return rc;
+    }
+    return VRHIP_OK;
+}
+extern "C" {
+
+static int refuse_multi(vrhip_ctx* c, const char* what)
+{
+    return fail(VRHIP_ERR_INVALID, std::string(what) + " is not available on a multi-device context (vrhip_create_multi)");
+}
+
+// every member's `what` tiles to the lead: pack on each member's stream, one
+// grouped ncclGather (one thread drives all ranks), unpack on the lead
+static int multi_gather(vrhip_ctx* c, int what)
+{
+    const size_t esz = what == 1 ? 16u : 4u;
+    const size_t bytes = (size_t)max_owned_pixels(c->W, c->H, (uint32_t)c->group.size()) * esz;
+    int rc;
+    for (vrhip_ctx* m : c->group) {
+        if ((rc = set_device(m)) != VRHIP_OK) return rc;
+        if ((rc = svc_close(m)) != VRHIP_OK) return rc;
+        if ((rc = vr::launch_pack_tiles(buf_of(m, what), m->comm_send, (uint32_t)esz, m->W, m->W / 16u,
+                                        owned_tiles_of(m->W, m->H, m->rank, m->nranks), m->rank, m->nranks, 0,
+                                        m->stream)) != 0)
+            return fail(VRHIP_ERR_HIP, "pack launch failed");
+    }
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+    for (vrhip_ctx* m : c->group) {
+        r = ncclGather(m->comm_send, m->comm_recv, bytes, ncclUint8, 0, m->comm, m->stream);
+        if (r != ncclSuccess) { (void)ncclGroupEnd(); return nccl_fail(r, "ncclGather"); }
+    }
+    r = ncclGroupEnd();
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
+    if ((rc = set_device(c)) != VRHIP_OK) return rc;
+    const uint32_t n = (uint32_t)c->group.size();
+    for (uint32_t rr = 1; rr < n; ++rr) {               // the lead's own tiles are in place
+        const uint32_t n_owned = owned_tiles_of(c->W, c->H, rr, n);
+        if (vr::launch_pack_tiles(c->comm_recv + (size_t)rr * bytes, const_cast<void*>(buf_of(c, what)), (uint32_t)esz,
+                                  c->W, c->W / 16u, n_owned, rr, n, 1, c->stream) != 0)
+            return fail(VRHIP_ERR_HIP, "unpack launch failed");
+    }
+    return VRHIP_OK;
+}
+
+int vrhip_create_multi(const int* devices, uint32_t n_devices, uint32_t width, uint32_t height, vrhip_ctx** out)
+{
+    if (!out || !devices || n_devices == 0 || n_devices > 64)
+        return fail(VRHIP_ERR_INVALID, "bad multi-device arguments (1..64 devices)");
+    *out = nullptr;
+    for (uint32_t i = 0; i < n_devices; ++i)
+        for (uint32_t j = 0; j < i; ++j)
+            if (devices[i] == devices[j]) return fail(VRHIP_ERR_INVALID, "a device appears twice");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(VRHIP_ERR_NO_DEVICE, "no HIP device");
+    for (uint32_t i = 0; i < n_devices; ++i)
+        if (devices[i] < 0 || devices[i] >= n) return fail(VRHIP_ERR_INVALID, "device index out of range");
+    std::vector<vrhip_ctx*> ms(n_devices, nullptr);
+    auto undo = [&](int code) {
+        for (vrhip_ctx* m : ms)
+            if (m) { m->group.clear(); vrhip_destroy(m); }
+        return code;
+    };
+    int rc;
+    for (uint32_t i = 0; i < n_devices; ++i) {
+        if ((rc = vrhip_create(devices[i], width, height, &ms[i])) != VRHIP_OK) return undo(rc);
+        ms[i]->service = 0;               // every render ends with the gather to the lead
+        ms[i]->rank = i; ms[i]->nranks = n_devices;
+    }
+    std::vector<ncclComm_t> comms(n_devices, nullptr);
+    const ncclResult_t r = ncclCommInitAll(comms.data(), (int)n_devices, devices);
+    if (r != ncclSuccess) return undo(nccl_fail(r, "ncclCommInitAll"));
+    const size_t slot = (size_t)max_owned_pixels(width, height, n_devices) * 16u;
+    for (uint32_t i = 0; i < n_devices; ++i) {
+        vrhip_ctx* m = ms[i];
+        m->comm = comms[i];
+        m->comm_rank = i; m->comm_n = n_devices; m->comm_slot = slot;
+        if ((rc = set_device(m)) != VRHIP_OK) return undo(rc);
+        if (hipMalloc((void**)&m->comm_send, slot ? slot : 16u) != hipSuccess ||
+            (i == 0 && hipMalloc((void**)&m->comm_recv, (slot ? slot : 16u) * n_devices) != hipSuccess))
+            return undo(fail(VRHIP_ERR_NOMEM, "gather buffers"));
+    }
+    ms[0]->group = ms;
+    (void)set_device(ms[0]);
+    *out = ms[0];
+    return VRHIP_OK;
+}
+
+int vrhip_device_group(vrhip_ctx* c, uint32_t* n_devices, int* devices)
+{
+    if (!c || !n_devices) return fail(VRHIP_ERR_INVALID, "null argument");
+    const uint32_t n = c->group.empty() ? 1u : (uint32_t)c->group.size();
+    if (devices)
+        for (uint32_t i = 0; i < n; ++i) devices[i] = c->group.empty() ? c->device : c->group[i]->device;
+    *n_devices = n;
+    return VRHIP_OK;
+}
+
+int vrhip_set_camera(vrhip_ctx* c, const float origin[3], const float dir[3], const float up[3], const float right[3],
+                     float fov_scale)
+{ return fanout(c, [&](vrhip_ctx* m) { return one_set_camera(m, origin, dir, up, right, fov_scale); }); }
+int vrhip_clear(vrhip_ctx* c) { return fanout(c, [&](vrhip_ctx* m) { return one_clear(m); }); }
+int vrhip_set_fresnel(vrhip_ctx* c, float coef, float power)
+{ return fanout(c, [&](vrhip_ctx* m) { return one_set_fresnel(m, coef, power); }); }
+int vrhip_use_cornell_box(vrhip_ctx* c, int e) { return fanout(c, [&](vrhip_ctx* m) { return one_use_cornell_box(m, e); }); }
+int vrhip_use_example_sphere(vrhip_ctx* c, int e) { return fanout(c, [&](vrhip_ctx* m) { return one_use_example_sphere(m, e); }); }
+int vrhip_set_strict_traversal(vrhip_ctx* c, int e) { return fanout(c, [&](vrhip_ctx* m) { return one_set_strict_traversal(m, e); }); }
+int vrhip_use_brdf(vrhip_ctx* c, int e) { return fanout(c, [&](vrhip_ctx* m) { return one_use_brdf(m, e); }); }
+int vrhip_upload_mesh_flat(vrhip_ctx* c, const float* bvh, size_t n_bvh_f4, const float* verts, const float* normals,
+                           const float* tangents, const float* uvs, size_t n_slots)
+{ return fanout(c, [&](vrhip_ctx* m) { return one_upload_mesh_flat(m, bvh, n_bvh_f4, verts, normals, tangents, uvs, n_slots); }); }
+int vrhip_upload_hdr(vrhip_ctx* c, const float* rgba, uint32_t w, uint32_t h)
+{ return fanout(c, [&](vrhip_ctx* m) { return one_upload_hdr(m, rgba, w, h); }); }
+int vrhip_upload_hdr_half(vrhip_ctx* c, const uint16_t* rgba_half, uint32_t w, uint32_t h)
+{ return fanout(c, [&](vrhip_ctx* m) { return one_upload_hdr_half(m, rgba_half, w, h); }); }
+int vrhip_upload_texture(vrhip_ctx* c, int type, const float* rgba, uint32_t w, uint32_t h)
+{ return fanout(c, [&](vrhip_ctx* m) { return one_upload_texture(m, type, rgba, w, h); }); }
+int vrhip_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
+{ return fanout(c, [&](vrhip_ctx* m) { return one_upload_brdf(m, table, n_floats); }); }
+int vrhip_set_overlap(vrhip_ctx* c, int mode) { return fanout(c, [&](vrhip_ctx* m) { return one_set_overlap(m, mode); }); }
+int vrhip_set_path_split(vrhip_ctx* c, uint32_t groups) { return fanout(c, [&](vrhip_ctx* m) { return one_set_path_split(m, groups); }); }
+int vrhip_set_service(vrhip_ctx* c, int mode)
+{
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_set_service");
+    return one_set_service(c, mode);
+}
+int vrhip_sync(vrhip_ctx* c) { return fanout(c, [&](vrhip_ctx* m) { return one_sync(m); }); }
+
+int vrhip_render(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed)
+{
+    if (!c || c->group.empty()) return one_render(c, n_frames, times, time_seed);
+    // every device renders its tiles (asynchronously), then the colour and
+    // depth tiles go to the lead
+    for (vrhip_ctx* m : c->group) {
+        const int rc = one_render(m, n_frames, times, time_seed);
+        if (rc != VRHIP_OK) return rc;
+    }
+    int rc = multi_gather(c, 0);
+    if (rc == VRHIP_OK) rc = multi_gather(c, 2);
+    return rc;
 }
 
 } // extern "C"

@@ -161,7 +161,10 @@ def default_fov_scale() -> float:
 class VRendererHIP:
     """MI355X peer of vRendererCuda behind the vRenderer interface."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device=0):
+        """device: a GPU index, or a sequence of them for one renderer over
+        several GPUs of this process (vrhip_create_multi: the tiles are dealt
+        over the devices, the images gathered to the first)."""
         self._lib = _native.lib()
         self._ctx = ctypes.c_void_p(None)
         self._device = device
@@ -176,7 +179,12 @@ class VRendererHIP:
         assert w != 0 and h != 0
         if self._ctx:
             self.cleanUp()
-        check(self._lib.vrhip_create(self._device, w, h, ctypes.byref(self._ctx)), "vrhip_create")
+        if isinstance(self._device, (list, tuple)):
+            devs = (ctypes.c_int * len(self._device))(*[int(d) for d in self._device])
+            check(self._lib.vrhip_create_multi(devs, len(self._device), w, h, ctypes.byref(self._ctx)),
+                  "vrhip_create_multi")
+        else:
+            check(self._lib.vrhip_create(self._device, w, h, ctypes.byref(self._ctx)), "vrhip_create")
         self.width, self.height = w, h
         check(self._lib.vrhip_set_fresnel(self._ctx, self.m_fresnelCoef, self.m_fresnelPow), "vrhip_set_fresnel")
 
@@ -337,6 +345,19 @@ class VRendererHIP:
     def set_overlap(self, mode: int) -> None:
         """Overlap of consecutive render launches: 1 always, 0 never, -1 automatic (vrhip_set_overlap)."""
         check(self._lib.vrhip_set_overlap(self._need_ctx(), int(mode)), "vrhip_set_overlap")
+
+    def device_group(self) -> list:
+        """The devices this renderer runs on (lead first; vrhip_device_group)."""
+        n = ctypes.c_uint32(0)
+        check(self._lib.vrhip_device_group(self._need_ctx(), ctypes.byref(n), None), "vrhip_device_group")
+        devs = (ctypes.c_int * n.value)()
+        check(self._lib.vrhip_device_group(self._ctx, ctypes.byref(n), devs), "vrhip_device_group")
+        return list(devs)
+
+    def set_service(self, mode: int) -> None:
+        """Render service sessions (consecutive launches on one persistent
+        kernel): 1 always, 0 never, -1 automatic (vrhip_set_service)."""
+        check(self._lib.vrhip_set_service(self._need_ctx(), int(mode)), "vrhip_set_service")
 
     def owned_pixels(self) -> int:
         """Pixels this rank renders (256 per owned 16x16 tile)."""
