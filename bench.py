@@ -67,6 +67,10 @@ WORKLOADS = {
     "C3": ("C3: HDRI env + 10k-tri torus knot with diffuse/normal/specular maps + Fresnel, 1280x720, "
            "2 spp/frame, 4 bounces",
            "synthetic (procedural 2048x1024 HDRI, 1024^2 maps, 10k-tri torus knot; SURVEY.md 8d C3)"),
+    "C2D": ("C2D (not a BASELINE config): C2 with a 1024^2 diffuse map on the knot, 1280x720, 2 spp/frame, 4 bounces",
+            "synthetic (procedural Cornell box + 10k-tri torus knot + diffuse map; feature-class kernel)"),
+    "C3D": ("C3D (not a BASELINE config): C3 with only the diffuse map, 1280x720, 2 spp/frame, 4 bounces",
+            "synthetic (procedural 2048x1024 HDRI, 1024^2 diffuse map, 10k-tri torus knot; feature-class kernel)"),
     "C4": ("C4: MERL BRDF on the example sphere under HDRI, 1920x1080 (rendered 1920x1072), 2 spp/frame, 4 bounces",
            "synthetic (procedural 2048x1024 HDRI, analytic lobe sampled on the MERL grid; SURVEY.md 8d C4)"),
     "C5": ("C5: 1M-tri torus knot (SBVH-depth tree) under HDRI, 3840x2160, 2 spp/frame, 4 bounces",

@@ -16,8 +16,8 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libvrhip.so")
 # the path kernels' scene specialisations are separate translation units
 # (vr_spec_*.hip) so that they compile in parallel
-SOURCES = ["vr_spec_generic.hip", "vr_spec_c2.hip", "vr_spec_c3.hip", "vr_spec_c5.hip", "vr_spec_c1.hip",
-           "vr_spec_c4.hip", "vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp", "vr_exr.cpp"]
+SOURCES = ["vr_spec_generic.hip", "vr_cls_cornell_mesh.hip", "vr_cls_hdri_mesh.hip", "vr_spec_c2.hip", "vr_spec_c3.hip", "vr_spec_c5.hip", "vr_spec_c1.hip",
+           "vr_spec_c4.hip", "vr_cls_sphere.hip", "vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp", "vr_exr.cpp"]
 HEADERS = ["vr_params.hpp", "vr_math.hpp", "vr_bvh.hpp", "vr_exr.hpp", "vr_kernel.hpp"]
 ARCH = os.environ.get("VRHIP_OFFLOAD_ARCH", "gfx950")
 

@@ -146,6 +146,21 @@ __global__ void selftest_math_kernel(int fn, const float* a, const float* b, flo
     out[i] = r;
 }
 
+// Flags outside the five exact specialisations -> their feature class
+// (vr_cls_*.hip), or the generic kernel (strict traversal).
+// VR_FEATURE_CLASSES=0 builds route them all to the generic kernel (A/B builds).
+#ifndef VR_FEATURE_CLASSES
+#define VR_FEATURE_CLASSES 1
+#endif
+static void launch_class(const RenderParams& p, uint32_t need, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode)
+{
+    const uint32_t cls = VR_FEATURE_CLASSES ? feature_class(need) : 0u;
+    if (cls == kClassCornellMesh) launch_cls_cornell_mesh(p, n_tiles, stack_depth, s, mode);
+    else if (cls == kClassHdriMesh) launch_cls_hdri_mesh(p, n_tiles, stack_depth, s, mode);
+    else if (cls == kClassCornellSphere || cls == kClassHdriSphere) launch_cls_sphere(p, n_tiles, stack_depth, s, mode);
+    else launch_spec_generic(p, n_tiles, stack_depth, s, mode);
+}
+
 // Scene flags -> specialisation (one translation unit each, vr_spec_*.hip).
 static void launch_scene(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, bool exec)
 {
@@ -156,7 +171,7 @@ static void launch_scene(const RenderParams& p, uint32_t n_tiles, int stack_dept
     else if (need == kFeatHdriMesh) launch_spec_c5(p, n_tiles, stack_depth, s, mode);
     else if (need == kFeatHdriMeshTex) launch_spec_c3(p, n_tiles, stack_depth, s, mode);
     else if (need == kFeatHdriBrdfSphere) launch_spec_c4(p, n_tiles, stack_depth, s, mode);
-    else launch_spec_generic(p, n_tiles, stack_depth, s, mode);
+    else launch_class(p, need, n_tiles, stack_depth, s, mode);
 }
 
 int launch_render(const RenderParams& p, uint32_t n_tiles, int stack_depth, int count, void* stream)
@@ -231,7 +246,7 @@ int launch_service(const RenderParams& p, uint32_t n_tiles, int stack_depth, voi
     if (need == kFeatCornellMesh) launch_spec_c2(p, n_tiles, stack_depth, s, 2);
     else if (need == kFeatHdriMesh) launch_spec_c5(p, n_tiles, stack_depth, s, 2);
     else if (need == kFeatHdriMeshTex) launch_spec_c3(p, n_tiles, stack_depth, s, 2);
-    else launch_spec_generic(p, n_tiles, stack_depth, s, 2);
+    else launch_class(p, need, n_tiles, stack_depth, s, 2);
     return (int)hipGetLastError();
 }
 

@@ -53,7 +53,16 @@ namespace vr {
 // F_EXACT are launched only when the scene's flags equal their feature set,
 // so their tests fold at compile time; the generic kernel tests the flags.
 constexpr uint32_t F_EXACT = 1u << 31;
-#define HAS(F) ((FEAT & (F)) != 0 && ((FEAT & F_EXACT) != 0 || (p.flags & (F)) != 0))
+// Feature-class specialisations (F_CLASS) are launched when the scene's
+// geometry flags (kClassGeom) equal theirs and its other flags are a subset
+// of FEAT: geometry tests fold at compile time, material features (texture
+// maps, BRDF view) are tested against the flags.  Every flag combination the
+// Qt UI produces on a mesh or sphere scene lands on one of them instead of the
+// generic kernel (vr_kernel.hip launch_scene).
+constexpr uint32_t F_CLASS = 1u << 30;
+constexpr uint32_t kClassGeom = 1u << 0 | 1u << 3;     // F_CORNELL | F_MESH
+#define HAS(F) ((FEAT & (F)) != 0 && ((FEAT & F_EXACT) != 0 || ((FEAT & F_CLASS) != 0 && ((F) & ~kClassGeom) == 0u) || \
+                                      (p.flags & (F)) != 0))
 
 // ---- float4 with the reference's operator semantics (MathHelpers.cuh:85-196)
 __device__ __forceinline__ vr4 mk4(float x, float y, float z, float w) { vr4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
@@ -250,9 +259,19 @@ struct Lds {
 constexpr int kSentinel = 0x76543210;
 struct Trav {
     float ivx, ivy, ivz, odx, ody, odz;
-    float t, tcull, bu, bv;
+    float t, tcull, bu, bv;   // tcull: read only by kernels with helper lanes (tcull_kept)
     int best, sp, nodeAddr;
 };
+// The culling distance is t x (1 + 2^-10) (infinite for the strict walk),
+// recomputed per node visit -- one v_mul against a register held through the
+// whole walk (C2 +0.5 %, C5 +0.5 %) -- except in the small-launch kernels,
+// whose helper lanes cull with the smaller of their own and their owner's
+// (help_step).
+#ifndef VR_TCULL_KEPT
+#define VR_TCULL_KEPT 0           // 1: every kernel keeps tcull in a register (A/B builds)
+#endif
+template <uint32_t FEAT>
+constexpr bool tcull_kept() { return VR_TCULL_KEPT != 0 || (FEAT & F_SMALL) != 0u; }
 
 template <uint32_t FEAT>
 __device__ __forceinline__ void trav_init(const RenderParams& p, const Ray& r, float t0, Trav& tr, const Lds& L)
@@ -298,6 +317,7 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
 {
     int* stk = L.stk;
     const bool strict = HAS(F_STRICT);   // compile-time false in the specialised kernels
+    const float tcull = tcull_kept<FEAT>() ? tr.tcull : strict ? __builtin_inff() : tr.t * 1.0009765625f;
     if (COUNT) cnt.nodes += 1u;
     if ((FEAT & F_SMALL) != 0u) cnt.work++;
     vr4 n0, n1, nz;
@@ -374,8 +394,8 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     // keep the child-index load in the same round trip as the bounds
     asm volatile("" ::"v"(idx0), "v"(idx1));
     const bool swp = (c1min < c0min);
-    const bool tc0 = (c0max >= c0min) && (c0min <= tr.tcull);
-    const bool tc1 = (c1max >= c1min) && (c1min <= tr.tcull);
+    const bool tc0 = (c0max >= c0min) && (c0min <= tcull);
+    const bool tc1 = (c1max >= c1min) && (c1min <= tcull);
     // branch-free push/pop: near child next, far child pushed when both
     // are hit, pop when neither is (same order as :324-343)
     const bool both = tc0 && tc1;
@@ -479,7 +499,7 @@ template <uint32_t FEAT>
 constexpr int node_break() {
     // one-frame kernels (F_INLINE_PRIM) keep 6: the interactive C2 rate fell
     // 2,147 -> 2,103 Mpaths/s with 10 (r02h)
-    return ((FEAT & F_EXACT) && (FEAT & F_CORNELL) && !(FEAT & F_INLINE_PRIM)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK;
+    return ((FEAT & (F_EXACT | F_CLASS)) && (FEAT & F_CORNELL) && !(FEAT & F_INLINE_PRIM)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK;
 }
 // The node-loop exit is proportional to the lanes in the call: a full wave
 // leaves once at most node_break of its 64 lanes still search (throughput:
@@ -1117,6 +1137,30 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
 template <uint32_t FEAT>
 constexpr bool prim_has_dir() { return (FEAT & F_EXAMPLE) == 0; }
 
+// The camera origin for a path that starts from its primary record.  The
+// 7-wave C2 kernel's only VGPR spills are vector copies of it (two scratch
+// stores per wave in the prologue, two reloads per refill: ~4 MB of the
+// launch's 996 MiB WRITE_SIZE, so not the write amplification -- DESIGN.md 5).
+// With VR_CAM_RELOAD it is reloaded from the kernel argument segment at the
+// point of use instead: 0 spills, but slower -- C2 -1.0 %, C3 -1.6 %, C5
+// -3.0 % (r04, scripts/ab.py): the allocator's other choices cost more than
+// the reloads did.  Off.
+#ifndef VR_CAM_RELOAD
+#define VR_CAM_RELOAD 0
+#endif
+static_assert(offsetof(RenderParams, cam_o) == 0, "cam_o leads the kernel argument");
+__device__ __forceinline__ vr4 cam_origin(const RenderParams& p)
+{
+#if VR_CAM_RELOAD
+    const vr4* k = (const vr4*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));                 // opaque: reloaded at every use
+    (void)p;
+    return *k;
+#else
+    return p.cam_o;
+#endif
+}
+
 // Primary hits, one thread per owned pixel: the camera ray's closest hit
 // (the HitRec intersect_scene returns: t, kind, idx, barycentrics,
 // example-sphere u,v), two float4s per pixel in the scratch order of
@@ -1557,7 +1601,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         hr.bv = b.x;
         if constexpr (prim_has_dir<FEAT>()) {
             hr.su = hr.sv = 0.f;
-            ray.o = p.cam_o;
+            ray.o = cam_origin(p);
             ray.d = mk4(b.y, b.z, b.w, (p.cam_d.w + p.cx.w) + p.cy.w);   // camera_ray's .w
         } else {
             hr.su = b.y; hr.sv = b.z;
@@ -1842,7 +1886,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
         hr.bv = b.x;
         if constexpr (prim_has_dir<FEAT>()) {
             hr.su = hr.sv = 0.f;
-            ray.o = p.cam_o;
+            ray.o = cam_origin(p);
             ray.d = mk4(b.y, b.z, b.w, (p.cam_d.w + p.cx.w) + p.cy.w);   // camera_ray's .w
         } else {
             hr.su = b.y; hr.sv = b.z;
@@ -1957,6 +2001,24 @@ constexpr uint32_t kFeatCornellSphere = F_CORNELL | F_EXAMPLE;                  
 constexpr uint32_t kFeatHdriMesh = F_MESH;                                                 // C5
 constexpr uint32_t kFeatHdriMeshTex = F_MESH | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;        // C3
 constexpr uint32_t kFeatHdriBrdfSphere = F_EXAMPLE | F_VIEW_BRDF | F_BRDF;                  // C4
+// Feature classes (F_CLASS): Cornell box or HDRI x mesh or spheres, any
+// material features (texture maps, BRDF view; the example sphere in the
+// sphere classes), no strict traversal.  The host never sets F_MESH with
+// F_EXAMPLE (the reference ignores the mesh then, PathTracer.cu:192,268).
+constexpr uint32_t kMaterialFeats = F_VIEW_BRDF | F_BRDF | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC;
+constexpr uint32_t kClassCornellMesh = F_CLASS | F_CORNELL | F_MESH | kMaterialFeats;
+constexpr uint32_t kClassHdriMesh = F_CLASS | F_MESH | kMaterialFeats;
+constexpr uint32_t kClassCornellSphere = F_CLASS | F_CORNELL | F_EXAMPLE | kMaterialFeats;
+constexpr uint32_t kClassHdriSphere = F_CLASS | F_EXAMPLE | kMaterialFeats;
+static_assert((kClassGeom & kMaterialFeats) == 0u && (kClassGeom & F_EXAMPLE) == 0u, "class geometry bits");
+// the feature class of a launch's flags (kFeatAll bits), 0: the generic kernel
+constexpr uint32_t feature_class(uint32_t need) {
+    return (need & F_STRICT) != 0u ? 0u
+         : (need & kClassGeom) == (F_CORNELL | F_MESH) ? ((need & F_EXAMPLE) ? 0u : kClassCornellMesh)
+         : (need & kClassGeom) == F_MESH ? ((need & F_EXAMPLE) ? 0u : kClassHdriMesh)
+         : (need & kClassGeom) == F_CORNELL ? kClassCornellSphere
+         : kClassHdriSphere;
+}
 
 // Multi-frame launches of fewer than 2^24 paths (shards) on the small-launch
 // kernels (F_SMALL: helper lanes, per-path costs, longest-first order) or,
@@ -2058,6 +2120,10 @@ void launch_spec_c3(const RenderParams& p, uint32_t n_tiles, int stack_depth, hi
 void launch_spec_c4(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
 void launch_spec_c5(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
 void launch_spec_generic(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
+// feature classes (kClass*): Cornell box + mesh, HDRI + mesh, and both sphere classes
+void launch_cls_cornell_mesh(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
+void launch_cls_hdri_mesh(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
+void launch_cls_sphere(const RenderParams& p, uint32_t n_tiles, int stack_depth, hipStream_t s, int mode);
 // trees deeper than 30 levels (64-entry stacks), production or instrumented
 void launch_spec_deep(const RenderParams& p, uint32_t n_tiles, hipStream_t s, bool exec);
 // the reference algorithm's counting variant (strict traversal, in place)

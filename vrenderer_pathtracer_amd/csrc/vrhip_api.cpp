@@ -1190,7 +1190,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     if (c->example) f |= vr::F_EXAMPLE;
     if (c->view_brdf) f |= vr::F_VIEW_BRDF;
     if (c->strict) f |= vr::F_STRICT;
-    if (c->mesh) f |= vr::F_MESH;
+    // the reference skips the mesh while the example sphere is on
+    // (PathTracer.cu:192,268): a sphere scene, whatever mesh is loaded
+    if (c->mesh && !c->example) f |= vr::F_MESH;
     if (c->brdf) f |= vr::F_BRDF;
     if (c->tex[0]) f |= vr::F_TEX_DIFF;
     if (c->tex[1]) f |= vr::F_TEX_NORM;

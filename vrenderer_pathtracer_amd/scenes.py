@@ -182,7 +182,7 @@ def knot_flat(nu: int, nv: int, max_leaf_tris: int = None) -> dict:
 
 
 def make_scene(config: str, width: int = None, height: int = None, knot=None) -> dict:
-    """Scene dict for C1..C5 (optionally at another resolution)."""
+    """Scene dict for C1..C5, C2D / C3D (optionally at another resolution)."""
     cfg = config.upper()
     sc = dict(camera=default_camera(), fresnel_coef=0.1, fresnel_pow=3.0, time=DEFAULT_TIME,
               cornell=False, example_sphere=False, view_brdf=False, name=cfg)
@@ -193,6 +193,15 @@ def make_scene(config: str, width: int = None, height: int = None, knot=None) ->
     elif cfg == "C3":
         sc.update(width=1280, height=720, hdr=procedural_hdr(), mesh_flat=knot_flat(*(knot or (100, 50))))
         sc.update(procedural_textures())
+    elif cfg == "C2D":
+        # not a BASELINE config: C2 with a diffuse map on the knot (a feature
+        # set outside the five exact specialisations: the Cornell-mesh class kernel)
+        sc.update(width=1280, height=720, cornell=True, mesh_flat=knot_flat(*(knot or (100, 50))))
+        sc.update(tex_diffuse=procedural_textures()["tex_diffuse"])
+    elif cfg == "C3D":
+        # not a BASELINE config: C3 with only the diffuse map (the HDRI-mesh class kernel)
+        sc.update(width=1280, height=720, hdr=procedural_hdr(), mesh_flat=knot_flat(*(knot or (100, 50))))
+        sc.update(tex_diffuse=procedural_textures()["tex_diffuse"])
     elif cfg == "C4":
         sc.update(width=1920, height=1080, hdr=procedural_hdr(), example_sphere=True, view_brdf=True,
                   brdf=synthetic_merl())
