@@ -439,10 +439,14 @@ def main():
         # scratch, 12-B path radiances + the 4-B depth term per pixel (+ the
         # 32-B primary records of mesh scenes) and the finish pass's accum /
         # RGBA8 / depth; in registers (sphere-only launches of one path group)
-        # only the accum / RGBA8 / depth of every pixel
+        # only the accum / RGBA8 / depth of every pixel.  A split sphere
+        # launch stores one 12-B record per pixel whose camera ray escapes
+        # (its paths share it: shared_miss_paths) instead of one per path
         store_bytes = 24 * owned
         if launch_info["use_scratch"]:
-            store_bytes += 12 * own_paths + 4 * owned + (32 * owned if mesh else 0)
+            shared = int(exec_counts.get("shared_miss_paths", 0))
+            store_bytes += (12 * (own_paths - shared) + 12 * (shared // (2 * F)) + 4 * owned
+                            + (32 * owned if mesh else 0))
         ref_b = reference_bytes(ref_counts, own_paths, owned * F)
         achieved = load_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         roofs = {}

@@ -25,7 +25,7 @@ if [ "$2" != "--no-tests" ]; then
   step smoke 120 python3 -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench_C2 300 python3 bench.py
-for cfg in C1 C3 C4 C5; do
+for cfg in C1 C3 C4 C5 C2D C3D; do
   step bench_$cfg 300 python3 bench.py --config $cfg --no-cpu
 done
 PB="bench.py --steps 5 --warmup 1 --no-cpu --no-roof --interactive-frames 0 --strong-steps 0"

@@ -26,11 +26,15 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     const uint32_t n_paths = 2u * p.n_frames;
     const uint32_t slot = tile * kBlockThreads + tid;
     const vr3* src = p.paths + slot;
-    const float depth = p.path_w[slot];
+    float depth = p.path_w[slot];
+    // a split sphere launch's escaped pixel: one result for all its paths
+    // (kSharedMissW; their depth term is 1, the miss at bounce 0)
+    const size_t qstride = depth == kSharedMissW ? 0u : (size_t)p.path_stride;
+    if (qstride == 0u) depth = 1.f;
     const bool cornell = (p.flags & F_CORNELL) != 0u;
     float last_w = 0.f;
     for (uint32_t q = 0; q < n_paths; ++q) {
-        const vr3 r = src[(size_t)q * p.path_stride];
+        const vr3 r = src[(size_t)q * qstride];
         last_w = (cornell && escaped(r.x)) ? 0.f : depth;
         io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
     }

@@ -990,6 +990,12 @@ __device__ __forceinline__ u8x4 tonemap(vr4 io, uint32_t frame) {
 // it and the escape mark -- a quarter less scratch written by the path
 // kernel and read by the (HBM-bound) finish pass.
 __device__ __forceinline__ bool escaped(float x) { return __float_as_uint(x) == 0x80000000u; }
+// Split sphere launches (render_kernel with RenderParams::split > 1): a pixel
+// whose camera ray escapes (shared_miss) has the same result for every path,
+// so group 0 stores it once -- paths[0][slot] -- and marks the pixel with a
+// depth term of -1 (a real one is >= 0); the other groups store nothing and
+// finish_kernel adds that one result for every path, in path order.
+constexpr float kSharedMissW = -1.0f;
 __device__ __forceinline__ void store_path(const RenderParams& p, uint32_t q, uint32_t slot, const vr4& out, float depth)
 {
     p.paths[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
@@ -1079,27 +1085,36 @@ __global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel
     // path) and the paths' sums below stay in path order, bit for bit the
     // same.  ~98 % of C4's paths (the sphere covers ~2 % of the image).
     const bool shared_miss = !ref_alg<COUNT, FEAT>() && !HAS(F_CORNELL) && !hit0;
+    // path q = 2*f + s (frame f of the launch, sample s); the seeds of a
+    // frame's second sample are its first sample's after one hash (:620-622)
+    const uint32_t n_paths = 2u * p.n_frames;
+    const uint32_t chunk = (n_paths + T - 1u) / T;
+    const uint32_t q0 = g * chunk < n_paths ? g * chunk : n_paths;
+    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
+    const bool direct = !p.use_scratch;                  // accumulate here (counting launches)
+    // split launches: an escaped pixel's group 0 stores its one record
+    // (kSharedMissW) and no group runs its paths
+    const bool one_record = shared_miss && !direct;
     vr4 miss_r = mk4(0.f, 0.f, 0.f, 0.f);
-    if (shared_miss) {
+    if (shared_miss && (direct || g == 0u)) {
         PathState ps;
         uint32_t d0 = 0, d1 = 0;                           // the miss branch draws no random number
         path_begin(ps, d0, d1);
         Ray r0 = cam;
         (void)bounce_step<COUNT, FEAT>(p, r0, hr0, ps, miss_r, cnt);
+        if (one_record) {
+            const uint32_t slot = tile * kBlockThreads + (uint32_t)tid;
+            p.paths[slot] = vr3{ miss_r.x, miss_r.y, miss_r.z };
+            p.path_w[slot] = kSharedMissW;
+        }
     }
-
-    // path q = 2*f + s (frame f of the launch, sample s); the seeds of a
-    // frame's second sample are its first sample's after one hash (:620-622)
-    const uint32_t n_paths = 2u * p.n_frames;
-    const uint32_t chunk = (n_paths + T - 1u) / T;
-    const uint32_t q0 = g * chunk;
-    const uint32_t q1 = q0 + chunk < n_paths ? q0 + chunk : n_paths;
-    const bool direct = !p.use_scratch;                  // accumulate here (counting launches)
+    if (COUNT && one_record) cnt.shared_miss += q1 - q0;
+    const uint32_t q_end = one_record ? q0 : q1;
     vr4 io = (direct && p.first_frame != 1u) ? p.accum[ind] : mk4(0.f, 0.f, 0.f, 0.f);
     uint32_t s1 = 0, s2 = 0;
     float last_w = 0.f;
 #pragma unroll 1
-    for (uint32_t q = q0; q < q1; ++q) {
+    for (uint32_t q = q0; q < q_end; ++q) {
         const uint32_t f = q >> 1;
         if ((q & 1u) == 0u || q == q0) {
             s1 = x * (p.first_frame + f);

@@ -897,7 +897,17 @@ static int take_event(vrhip_ctx* c, hipEvent_t* e)
 // 4 0.639, 8 0.678; one frame per call 0.089 ms against 0.105-0.145; C1
 // (1,024 tiles) split 1 0.434, 2 0.319, 4 0.296, 8 0.299, 16 0.310; one frame
 // per call 0.062 (split 1) against 0.068.
-static uint32_t choose_split(const vrhip_ctx* c, uint32_t n_tiles, uint32_t k)
+// Sphere-only HDRI scenes (C4): path groups per pixel at least this many.
+// Their pixels split into camera-ray escapes -- one result for all paths,
+// stored once (kSharedMissW) -- and the few on the example sphere, whose 2K
+// paths (BRDF lookups, HDRI fetches: dependent gathers) one thread would run
+// back to back, the launch's critical path.  C4 at 16 frames per launch
+// (r04, scripts/c4_probe.py): 1 group 0.470 ms, 2 0.323, 4 0.246, 8 0.253,
+// 16 0.362 (every group recomputes the camera ray and sphere tests).
+#ifndef VR_SPHERE_SPLIT
+#define VR_SPHERE_SPLIT 4
+#endif
+static uint32_t choose_split(const vrhip_ctx* c, uint32_t n_tiles, uint32_t k, bool shared_escape)
 {
     uint32_t t = c->path_split;
     if (t == 0) {
@@ -905,6 +915,7 @@ static uint32_t choose_split(const vrhip_ctx* c, uint32_t n_tiles, uint32_t k)
         t = 1;
         if (k > 1)
             while (n_tiles * t < target && t < 2u * k) t *= 2;
+        if (shared_escape) t = std::max<uint32_t>(t, VR_SPHERE_SPLIT);
     }
     return std::max<uint32_t>(1u, std::min<uint32_t>(t, 2u * k));
 }
@@ -1214,7 +1225,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         p.counters = c->counters;
     }
     const uint32_t k_max = std::min<uint32_t>(n_frames, (uint32_t)vr::kMaxFramesPerLaunch);
-    const uint32_t split_max = count == 1 ? 1u : choose_split(c, n_tiles, k_max);
+    // sphere-only HDRI scenes: camera-ray escapes share one result (render_kernel)
+    const bool shared_escape = (f & (vr::F_MESH | vr::F_CORNELL)) == 0u;
+    const uint32_t split_max = count == 1 ? 1u : choose_split(c, n_tiles, k_max, shared_escape);
     p.path_stride = n_tiles * (uint32_t)vr::kBlockThreads;
     const size_t need = (size_t)2 * k_max * p.path_stride;   // scratch float4s of the largest launch
     // the path-pool kernel is persistent: one resident set of blocks per CU
