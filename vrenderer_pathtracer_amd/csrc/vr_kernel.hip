@@ -26,17 +26,22 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     const uint32_t n_paths = 2u * p.n_frames;
     const uint32_t slot = tile * kBlockThreads + tid;
     const vr3* src = p.paths + slot;
-    float depth = p.path_w[slot];
-    // a split sphere launch's escaped pixel: one result for all its paths
-    // (kSharedMissW; their depth term is 1, the miss at bounce 0)
-    const size_t qstride = depth == kSharedMissW ? 0u : (size_t)p.path_stride;
-    if (qstride == 0u) depth = 1.f;
+    const float depth = p.path_w[slot];
     const bool cornell = (p.flags & F_CORNELL) != 0u;
     float last_w = 0.f;
-    for (uint32_t q = 0; q < n_paths; ++q) {
-        const vr3 r = src[(size_t)q * qstride];
-        last_w = (cornell && escaped(r.x)) ? 0.f : depth;
-        io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
+    if (depth == kSharedMissW) {
+        // a split sphere launch's escaped pixel: one result for all its paths
+        // (their depth term is 1, the miss at bounce 0), added path by path
+        const vr3 r = src[0];
+        const vr4 h = mul4s(mk4(r.x, r.y, r.z, 1.f), 1.f / 2.f);
+        for (uint32_t q = 0; q < n_paths; ++q) io = add4(io, h);
+        last_w = 1.f;
+    } else {
+        for (uint32_t q = 0; q < n_paths; ++q) {
+            const vr3 r = src[(size_t)q * p.path_stride];
+            last_w = (cornell && escaped(r.x)) ? 0.f : depth;
+            io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
+        }
     }
     const unsigned char db = f2u8((1.f - last_w) * 255);
     u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;

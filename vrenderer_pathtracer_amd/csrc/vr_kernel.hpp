@@ -948,7 +948,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
 }
 
 template <int STACK, bool COUNT, uint32_t FEAT>
-__device__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit0, uint32_t& s0, uint32_t& s1,
+__device__ __forceinline__ vr4 trace(const RenderParams& p, Ray ray, const HitRec& hr0, bool hit0, uint32_t& s0, uint32_t& s1,
                      const Lds& L, Cnt& cnt, float& depth)
 {
     PathState ps;
