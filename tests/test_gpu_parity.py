@@ -214,7 +214,7 @@ def test_c5_tree_bitexact_vs_portable_oracle(native, oracle, cfg, w, h):
 
 
 @pytest.mark.parametrize("cfg,w,h,frames", [("C2", 160, 96, 3), ("C3", 160, 96, 2), ("C4", 144, 96, 2),
-                                            ("C5", 96, 64, 2), ("C1", 96, 96, 3)])
+                                            ("C4", 144, 96, 8), ("C5", 96, 64, 2), ("C1", 96, 96, 3)])
 def test_profiled_render_is_the_production_render(native, cfg, w, h, frames):
     """vrhip_render_profiled (the instrumented copy of the production kernels
     that the roofline's executed bytes come from) renders the same bits as
@@ -360,6 +360,35 @@ def test_path_split_is_result_invariant(native, cfg, frames):
         assert_bitexact(got[0], base[0], sc, f"accum split={split}")
         assert_bitexact(got[1], base[1], sc, f"rgba split={split}")
         assert_bitexact(got[2], base[2], sc, f"depth split={split}")
+
+
+@pytest.mark.parametrize("cfg,w,h,frames,tiling", [("C4", 144, 96, 8, None), ("C4", 96, 64, 70, None),
+                                                    ("C4", 144, 96, 6, (1, 3)), ("C4", 400, 240, 4, None)])
+def test_split_sphere_launch_bitexact_vs_portable_oracle(native, oracle, cfg, w, h, frames, tiling):
+    """Sphere-only HDRI scenes, launches of >= 4 frames: each pixel's paths in
+    4 path groups (VR_SPHERE_SPLIT), an escaped pixel's one shared result
+    stored once (kSharedMissW) -- equal to the oracle and to render_kernel's
+    direct accumulation (one path group) bit for bit, also over several
+    launches (70 frames) and on a tiled rank."""
+    sc = scenes.make_scene(cfg, w, h)
+    times = [sc["time"] + 5 * i for i in range(frames)]
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    if tiling:
+        r.set_tiling(*tiling)
+    r.render(frames=frames, times=times)
+    info = r.last_launch_info()
+    got = r.read_accum(), r.read_rgba8(), r.read_depth8()
+    r.cleanUp()
+    assert info["kind"] == "render_kernel" and info["use_scratch"] == 1 and info["split"] >= 4, info
+    direct = gpu_render(sc, frames, times, tiling=tiling, split=1)
+    for g, b, what in zip(got, direct, ("accum", "rgba8", "depth8")):
+        assert_bitexact(g, b, sc, f"{what} vs one path group")
+    if tiling is None:
+        oa, orgba, od, _ = po.render(sc, frames=frames, times=times, libm=po.LIBM_PORTABLE)
+        assert_bitexact(got[0], oa, sc, "accum vs oracle")
+        assert_bitexact(got[1], orgba, sc, "rgba8 vs oracle")
+        assert_bitexact(got[2], od, sc, "depth8 vs oracle")
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C5"])

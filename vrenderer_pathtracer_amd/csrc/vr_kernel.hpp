@@ -802,6 +802,29 @@ __device__ __forceinline__ void path_begin(PathState& ps, uint32_t& s0, uint32_t
     ps.rng.seed(hash_seeds(s0, s1));
 }
 
+// Coherence probe (-DVR_PROBE_COHERENT=G; INVALID images, measurement only):
+// the lanes sampling a diffuse / BRDF bounce in the same step are split into
+// G groups of 64/G lanes, and every lane takes its group leader's (first
+// active lane's) direction sample -- G = 1: one sample per wave-step (the
+// ideal bound), G = 64: no change.  Bounds what binning bounce rays by
+// direction could return at a given number of distinct directions per wave
+// (C2, r04: G = 1 +15.3 %, G = 4 +3.7 %, G = 16 +0.5 %).
+__device__ __forceinline__ void probe_coherent(float& rand1, float& rand2)
+{
+#ifdef VR_PROBE_COHERENT
+    constexpr int G = VR_PROBE_COHERENT, span = 64 / G;
+    const int lane = (int)__lane_id();
+    const unsigned long long act = __ballot(1);
+    const int g0 = (lane / span) * span;
+    const unsigned long long grp = (span == 64 ? ~0ull : ((1ull << span) - 1ull)) << g0;
+    const int leader = __builtin_ctzll(act & grp);
+    rand1 = __shfl(rand1, leader, 64);
+    rand2 = __shfl(rand2, leader, 64);
+#else
+    (void)rand1; (void)rand2;
+#endif
+}
+
 // One bounce of trace's loop body (:627-769) for the closest hit `hr` of
 // `ray` (hr.t == 1e20: miss).  Returns true when the path ends, with its
 // radiance (w = depth) in `out`; otherwise `ray` is the next bounce's ray.
@@ -899,6 +922,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         } else {
             float rand1 = 2.f * VR_PI * ps.rng.uniform();
             float rand2 = ps.rng.uniform();
+            probe_coherent(rand1, rand2);
             const float rand2s = sqrt_exact(rand2);
             const vr4 u = normalize4(cross4(axis, w));
             const vr4 v = cross4(w, u);
@@ -917,6 +941,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
         float rand1 = 2.f * VR_PI * ps.rng.uniform();
         float rand2 = ps.rng.uniform();
+        probe_coherent(rand1, rand2);
         const float rand2s = sqrt_exact(rand2);
         const vr4 u = normalize4(cross4(axis, w));
         const vr4 v = cross4(w, u);
