@@ -1,9 +1,35 @@
 #!/bin/bash
-# VGPRs / spills of the production path-kernel specialisations in a
-# build_variants log:  bash scripts/kres.sh variants/<name>.log
-for k in "16ELj2147483657ELi256:C2-16f" "16ELj2147508233ELi256:C2-1f" "16ELj2147500041ELi256:C2-shard" \
-         "16ELj2147483880ELi768:C3-16f" "16ELj2147508456ELi256:C3-1f" "16ELj2147500264ELi256:C3-shard" \
-         "24ELj2147483656ELi768:C5-16f" "24ELj2147500040ELi256:C5-shard"; do
-  n=${k%%:*}; lab=${k#*:}
-  echo "$lab: $(grep -A14 "render_wave_kernelILi${n}EEEvNS_12RenderParamsE" $1 | grep -E "VGPRs:|VGPRs Spill|SGPRs Spill|ScratchSize" | sed 's/.*remark: *//;s/ \[-Rpass.*//' | tr '\n' ' ')"
-done
+# VGPRs / spills / scratch of the production path-kernel instantiations in a
+# build_variants log (kernel-resource-usage remarks):
+#   bash scripts/kres.sh variants/<name>.log
+python3 - "$1" <<'PY'
+import re, sys
+recs, cur = {}, None
+for line in open(sys.argv[1]):
+    m = re.search(r"Function Name: (\S+)", line)
+    if m:
+        cur = recs.setdefault(m.group(1), {})
+        continue
+    m = re.search(r"remark:\s+(VGPRs|VGPRs Spill|SGPRs Spill|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\d+)", line)
+    if m and cur is not None and m.group(1) not in cur:
+        cur[m.group(1)] = int(m.group(2))
+E, INL, SML, SVC = 2147483648, 8192, 16384, 32768
+C2, C3, C5 = E + 9, E + 232, E + 8
+CLS_C, CLS_H = (1 << 30) + 253, (1 << 30) + 252
+rows = [("C2 whole frame", "render_wave_kernel", 16, C2, 256), ("C2 one frame", "render_wave_kernel", 16, C2 + INL + SML, 256),
+        ("C2 service", "render_service_kernel", 16, C2 + SVC, 256),
+        ("C3 whole frame", "render_wave_kernel", 16, C3, 768), ("C3 shard", "render_wave_kernel", 16, C3, 256),
+        ("C3 one frame", "render_wave_kernel", 16, C3 + INL + SML, 256), ("C3 service", "render_service_kernel", 16, C3 + SVC, 256),
+        ("C5 whole frame", "render_wave_kernel", 24, C5, 768), ("C5 shard", "render_wave_kernel", 24, C5, 256),
+        ("C5 service", "render_service_kernel", 24, C5 + SVC, 256),
+        ("class Cornell+mesh", "render_wave_kernel", 16, CLS_C, 768), ("class HDRI+mesh", "render_wave_kernel", 16, CLS_H, 768)]
+print(f"{'kernel':22s} {'VGPRs':>5s} {'spill':>5s} {'scratch':>7s} {'waves':>5s}")
+for lab, k, st, feat, bt in rows:
+    name = f"_ZN2vr{len(k)}{k}ILi{st}ELj{feat}ELi{bt}EEEvNS_12RenderParamsE"
+    r = recs.get(name)
+    if r is None:
+        print(f"{lab:22s} (not in this build)")
+        continue
+    print(f"{lab:22s} {r.get('VGPRs', 0):5d} {r.get('VGPRs Spill', 0):5d} {r.get('ScratchSize [bytes/lane]', 0):7d} "
+          f"{r.get('Occupancy [waves/SIMD]', 0):5d}")
+PY
