@@ -29,5 +29,6 @@ for split in (None, 1, 2, 4, 8, 16):
     ms, rate = timed(sc, split)
     print(f"C4 split {split}: {ms:.4f} ms/step  {rate:10.1f} Mpaths/s", flush=True)
 no = dict(sc); no.update(example_sphere=False, view_brdf=False, brdf=None)
-ms, rate = timed(no)
-print(f"C4 without the sphere (all pixels escape): {ms:.4f} ms/step  {rate:10.1f} Mpaths/s", flush=True)
+for split in (None, 1, 2, 4):
+    ms, rate = timed(no, split)
+    print(f"C4 without the sphere (all pixels escape), split {split}: {ms:.4f} ms/step  {rate:10.1f} Mpaths/s", flush=True)

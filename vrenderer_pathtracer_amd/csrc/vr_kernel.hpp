@@ -1074,11 +1074,23 @@ __device__ __forceinline__ Ray camera_ray(const RenderParams& p, uint32_t x, uin
 #endif
 // 64-entry stacks take 64 KiB of LDS per 256 threads: at most 2 waves/SIMD
 constexpr int min_waves(int stack) { return stack > 32 ? 2 : VR_MIN_WAVES_PER_SIMD; }
+// Sphere-only kernels (no F_MESH in FEAT: C1, C4 and the sphere classes) have
+// no traversal stack or node cache in LDS, and ask for this many waves per
+// SIMD: their paths are chains of dependent gathers (BRDF table, HDRI) and
+// portable-libm transcendentals.  r04 (`scripts/ab.py`, against the kernels
+// with the mesh kernels' 40-KB LDS footprint, 4 waves): 4 / 6 / 8 waves C4
+// +2.0 / +1.6 / -14.5 %, C1 +2.1 / +4.4 / +2.7 % (8: 17 and 6 VGPRs spilled).
+#ifndef VR_SPHERE_MIN_WAVES
+#define VR_SPHERE_MIN_WAVES 6
+#endif
+template <uint32_t FEAT>
+constexpr int render_waves(int stack) { return (FEAT & F_MESH) != 0u ? min_waves(stack) : VR_SPHERE_MIN_WAVES; }
 template <int STACK, bool COUNT, uint32_t FEAT>
-__global__ void __launch_bounds__(kBlockThreads, min_waves(STACK)) render_kernel(const RenderParams p)
+__global__ void __launch_bounds__(kBlockThreads, render_waves<FEAT>(STACK)) render_kernel(const RenderParams p)
 {
-    constexpr int CN = cache_nodes(STACK);
-    __shared__ int lds_stack[STACK * kBlockThreads];
+    constexpr bool MK = (FEAT & F_MESH) != 0u;           // a kernel that may traverse the mesh
+    constexpr int CN = MK ? cache_nodes(STACK) : 1;
+    __shared__ int lds_stack[MK ? STACK * kBlockThreads : 1];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
     const int tid = threadIdx.x;
