@@ -13,7 +13,10 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
     // the path kernel's queue heads, for the next launch on this scratch
     if (tile == 0 && tid <= VR_MAX_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride] = 0u;
-    if (tile == 0 && tid == VR_MAX_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride + 1u] = 0u;   // drained-queue mask
+    if (tile == 0 && tid == VR_MAX_QUEUES && p.chunk_ctr) {
+        p.chunk_ctr[tid * kQueueStride + 1u] = 0u;      // drained-queue mask
+        *sparse_count_of(p.chunk_ctr) = 0u;            // an F_SPARSE launch's sub-tile list
+    }
     const int wave = (int)tid >> 6, lane = (int)tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
     const uint32_t tile_y = gtile / p.tiles_x;

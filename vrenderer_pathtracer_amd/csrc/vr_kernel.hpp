@@ -1021,6 +1021,8 @@ __device__ __forceinline__ bool escaped(float x) { return __float_as_uint(x) == 
 // depth term of -1 (a real one is >= 0); the other groups store nothing and
 // finish_kernel adds that one result for every path, in path order.
 constexpr float kSharedMissW = -1.0f;
+// The listed sub-tile count of an F_SPARSE launch, after the drained-queue mask.
+__device__ __forceinline__ uint32_t* sparse_count_of(uint32_t* chunk_ctr) { return chunk_ctr + VR_MAX_QUEUES * kQueueStride + 2u; }
 __device__ __forceinline__ void store_path(const RenderParams& p, uint32_t q, uint32_t slot, const vr4& out, float depth)
 {
     p.paths[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
@@ -1183,6 +1185,15 @@ __global__ void __launch_bounds__(kBlockThreads, render_waves<FEAT>(STACK)) rend
     if (COUNT) flush_counts(p, cnt, lane, (FEAT & F_COUNT_EXEC) != 0u);
 }
 
+// Specialisations that may run F_SPARSE launches: HDRI mesh scenes (an
+// escaped camera ray ends the path at once), exact or feature-class kernels,
+// multi-frame launches with a primary pass.
+template <uint32_t FEAT>
+constexpr bool sparse_ok() {
+    return (FEAT & F_MESH) != 0u && (FEAT & F_CORNELL) == 0u && (FEAT & (F_EXACT | F_CLASS)) != 0u &&
+           (FEAT & (F_INLINE_PRIM | F_SMALL | F_SERVICE)) == 0u;
+}
+
 // Kernels without the example sphere (whose hits need the u,v slots) store
 // the camera ray's direction in the primary record instead, so a path starts
 // without recomputing it (two f64 divisions and a normalisation).
@@ -1240,13 +1251,37 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
     Cnt cnt;
     HitRec hr;
     const Ray cam = camera_ray(p, x, y);
-    (void)intersect_scene<STACK, CNT, FEAT>(p, cam, hr, L, cnt);
-    vr4* dst = p.prim + 2u * ((size_t)tile * kBlockThreads + tid);
+    const bool hit = intersect_scene<STACK, CNT, FEAT>(p, cam, hr, L, cnt);
+    const uint32_t slot = tile * kBlockThreads + (uint32_t)tid;
+    vr4* dst = p.prim + 2u * (size_t)slot;
     dst[0] = mk4(hr.t, __int_as_float(hr.kind), __int_as_float(hr.idx), hr.bu);
     if constexpr (prim_has_dir<FEAT>())
         dst[1] = mk4(hr.bv, cam.d.x, cam.d.y, cam.d.z);   // the paths reuse the camera ray too
     else
         dst[1] = mk4(hr.bv, hr.su, hr.sv, 0.f);
+    if constexpr (sparse_ok<FEAT>()) {
+        if (p.sparse_subs) {
+            // F_SPARSE launch: an escaped camera ray gives every path of the
+            // pixel the same result (render_kernel's shared escape), stored
+            // once; the sub-tile joins the path kernel's list if any of its
+            // pixels hit the scene
+            if (!hit) {
+                PathState ps;
+                uint32_t d0 = 0, d1 = 0;                   // the miss branch draws no random number
+                path_begin(ps, d0, d1);
+                Ray r0 = cam;
+                vr4 miss_r;
+                (void)bounce_step<CNT, FEAT>(p, r0, hr, ps, miss_r, cnt);
+                p.paths[slot] = vr3{ miss_r.x, miss_r.y, miss_r.z };
+                p.path_w[slot] = kSharedMissW;
+                if (CNT) cnt.shared_miss += 2u * p.n_frames;
+            }
+            if (__ballot(hit) != 0ull && lane == 0) {
+                const uint32_t at = atomicAdd(sparse_count_of(p.chunk_ctr), 1u);
+                p.sparse_subs[at] = slot >> 6;
+            }
+        }
+    }
     if (CNT) flush_counts(p, cnt, lane, true);
 }
 
@@ -1534,7 +1569,9 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
     const uint32_t n_paths = 2u * p.n_frames;
-    const uint32_t n_sub = p.path_stride >> 6;             // 8x8 sub-tiles of the rank's tiles
+    constexpr bool SPARSE = (FEAT & F_SPARSE) != 0u;       // the listed sub-tiles only
+    // 8x8 sub-tiles of the rank's tiles, or the F_SPARSE list of those holding a hit
+    const uint32_t n_sub = SPARSE ? __builtin_amdgcn_readfirstlane(*sparse_count_of(p.chunk_ctr)) : p.path_stride >> 6;
     constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;      // instrumented copy (vrhip_render_profiled)
     Cnt cnt;
 
@@ -1562,6 +1599,10 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             if (lane == 0) v = atomicAdd(p.chunk_ctr + qj * kQueueStride, 1u);
             const uint32_t sb = queue_item(qj, __builtin_amdgcn_readfirstlane(v), Q, n_paths, path);
             if (sb < n_sub) {
+                if constexpr (SPARSE) {                    // the listed sub-tile
+                    sub = __builtin_amdgcn_readfirstlane(p.sparse_subs[sb]);
+                    return;
+                }
 #if VR_XCD_BANDS
                 // longest-first: the XCD's sub-tiles in the order of the
                 // previous launch's cost (order_kernel); else band order
@@ -1651,6 +1692,11 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
         hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
         hr.bv = b.x;
+        if constexpr (SPARSE) {
+            // an escaped pixel of a listed sub-tile: its shared result is
+            // stored (primary_kernel); the lane takes the next item
+            if (hr.kind == HK_NONE) { state = LS_DONE; return; }
+        }
         if constexpr (prim_has_dir<FEAT>()) {
             hr.su = hr.sv = 0.f;
             ray.o = cam_origin(p);
@@ -1729,6 +1775,8 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 state = LS_SETUP;
             }
         }
+        // (F_SPARSE: lanes whose item was an escaped pixel take another)
+        if constexpr (SPARSE) ended = ended || (state == LS_DONE && cur_sub != ~0u);
         const unsigned long long em = __ballot(ended);
         if (em != 0ull) {
             const uint32_t need = (uint32_t)__popcll(em);
@@ -1743,7 +1791,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             if (next + need > 64u) { cur_sub = nsub; cur_q = nq; next = next + need - 64u; }
             else next += need;
         }
-        if (__ballot(state != LS_DONE) == 0ull) break;
+        if (__ballot(state != LS_DONE) == 0ull && (!SPARSE || cur_sub == ~0u)) break;
     }
     if (CNT) flush_counts(p, cnt, lane, true);
 }
@@ -2109,6 +2157,18 @@ inline void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
         const uint32_t capped = p.waves_cap * 4u * 64u / (uint32_t)bt;
         return capped < 1u ? 1u : (capped < full ? capped : full);
     };
+    if constexpr (sparse_ok<FEAT>()) {
+        if (p.sparse_subs) {                      // the listed sub-tiles only (same shape and residency)
+            const int bt = (B == 0 && p.small_blocks) ? BTS : BT;
+            if (bt == BTS)
+                hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT | F_SPARSE, BTS>), dim3(p.wave_blocks * per_cu(BTS)),
+                                   dim3(BTS), 0, s, p);
+            else
+                hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT | F_SPARSE, BT>), dim3(p.wave_blocks * per_cu(BT)),
+                                   dim3(BT), 0, s, p);
+            return;
+        }
+    }
     if constexpr (B == 0) {
         if (p.small_blocks) {
             hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT, BTS>), dim3(p.wave_blocks * per_cu(BTS)), dim3(BTS), 0, s, p);

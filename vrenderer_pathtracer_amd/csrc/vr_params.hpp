@@ -41,6 +41,12 @@ enum Flags : uint32_t {
     // consecutive launches of a session from a descriptor ring, tagged
     // primary records, results per launch slot (vrhip_api.cpp Session)
     F_SERVICE = 1u << 15,
+    // compile-time only: the path kernel of HDRI mesh launches that skip the
+    // pixels whose camera ray escapes (RenderParams::sparse_subs): the
+    // primary pass stores each such pixel's one shared result and lists the
+    // 8x8 sub-tiles holding a camera-ray hit; the path kernel runs the paths
+    // of the listed sub-tiles only
+    F_SPARSE = 1u << 16,
 };
 constexpr int kMaxFramesPerLaunch = 64;
 
@@ -182,6 +188,10 @@ struct RenderParams {
     size_t svc_slot_bytes;           // result scratch per launch slot: 2 svc_kmax rows of path_stride vr3, then path_w
     uint32_t svc_kmax;               // frames per launch a slot holds
     uint32_t svc_idle_ticks;         // 100 MHz ticks with no new launch after which the service retires
+    // F_SPARSE launches (nullptr otherwise): the sub-tiles holding a
+    // camera-ray hit, appended by primary_kernel (their count at
+    // sparse_count_of(chunk_ctr), reset by finish_kernel)
+    uint32_t* sparse_subs;
     uint32_t times[kMaxFramesPerLaunch];
 };
 

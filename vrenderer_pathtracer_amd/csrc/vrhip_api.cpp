@@ -907,6 +907,11 @@ static int take_event(vrhip_ctx* c, hipEvent_t* e)
 #ifndef VR_SPHERE_SPLIT
 #define VR_SPHERE_SPLIT 4
 #endif
+// HDRI mesh launches with a primary pass: escaped camera rays' pixels take
+// one shared result and leave the path kernel (F_SPARSE; 0: every path runs, A/B builds)
+#ifndef VR_SPARSE_HDRI
+#define VR_SPARSE_HDRI 1
+#endif
 static uint32_t choose_split(const vrhip_ctx* c, uint32_t n_tiles, uint32_t k, bool shared_escape)
 {
     uint32_t t = c->path_split;
@@ -1314,6 +1319,11 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         const bool ovl = count == 0 && (c->overlap > 0 || (c->overlap < 0 && ovl_size && in_flight));
         p.small_blocks = small ? 1u : 0u;
         p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
+        // HDRI mesh launches with a primary pass skip the pixels whose camera
+        // ray escapes: one shared result each, the path kernel over the
+        // sub-tiles holding a hit (F_SPARSE, vr_kernel.hpp primary_kernel)
+        const bool sparse = VR_SPARSE_HDRI != 0 && wave_kernel && !c->cornell && count != 1 &&
+                            (f & vr::F_STRICT) == 0u && !p.inline_prim;
         p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? (c->cornell ? VR_QUEUES : VR_QUEUES_HDRI)
                                                                         : VR_QUEUES_LARGE;
         // VRHIP_QUEUES: work-queue heads for experiments (a power of two, 8..VR_MAX_QUEUES)
@@ -1346,6 +1356,10 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = reinterpret_cast<vr::vr3*>(l.paths); p.path_w = reinterpret_cast<float*>(p.paths + need);
             p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
+            // the F_SPARSE sub-tile list lives in the order buffer, which a
+            // later one-frame launch on this scratch then must not take as an order
+            p.sparse_subs = sparse ? l.sub_order : nullptr;
+            if (sparse) l.order_nsub = 0;
             // longest-first: launches whose drain is a large share of them (one
             // frame per call, shards) measure per sub-tile costs and take their
             // sub-tiles in the order the previous launch on this scratch measured
