@@ -221,15 +221,28 @@ __global__ void __launch_bounds__(kBlockThreads) svc_finish_kernel(const RenderP
     const bool cornell = (p.flags & F_CORNELL) != 0u;
     uint32_t frame = f.first_frame;
     float last_w = 0.f;
+    // an F_SPARSE session's escaped pixel: its one result for every path of
+    // every launch, in its primary record (primary_kernel), depth term 1
+    const bool shared = p.sparse_subs && __float_as_int(p.prim[2u * slot].y) == (int)HK_NONE;
+    vr4 shared_h = mk4(0.f, 0.f, 0.f, 0.f);
+    if (shared) {
+        const vr4 b = p.prim[2u * slot + 1u];
+        shared_h = mul4s(mk4(b.y, b.z, b.w, 1.f), 1.f / 2.f);
+    }
     for (uint32_t L = 0; L < f.n; ++L) {
         const vr3* base = reinterpret_cast<const vr3*>(reinterpret_cast<const uint8_t*>(p.paths) + (size_t)L * p.svc_slot_bytes);
-        const float depth = reinterpret_cast<const float*>(base + (size_t)2u * p.svc_kmax * p.path_stride)[slot];
-        const vr3* src = base + slot;
         const uint32_t n_paths = 2u * f.n_frames[L];
-        for (uint32_t q = 0; q < n_paths; ++q) {
-            const vr3 r = src[(size_t)q * p.path_stride];
-            last_w = (cornell && escaped(r.x)) ? 0.f : depth;
-            io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
+        if (shared) {
+            for (uint32_t q = 0; q < n_paths; ++q) io = add4(io, shared_h);
+            last_w = 1.f;
+        } else {
+            const float depth = reinterpret_cast<const float*>(base + (size_t)2u * p.svc_kmax * p.path_stride)[slot];
+            const vr3* src = base + slot;
+            for (uint32_t q = 0; q < n_paths; ++q) {
+                const vr3 r = src[(size_t)q * p.path_stride];
+                last_w = (cornell && escaped(r.x)) ? 0.f : depth;
+                io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
+            }
         }
         frame += f.n_frames[L];
         if (f.gather[L]) {

@@ -1021,8 +1021,13 @@ __device__ __forceinline__ bool escaped(float x) { return __float_as_uint(x) == 
 // depth term of -1 (a real one is >= 0); the other groups store nothing and
 // finish_kernel adds that one result for every path, in path order.
 constexpr float kSharedMissW = -1.0f;
-// The listed sub-tile count of an F_SPARSE launch, after the drained-queue mask.
+// The listed sub-tile count of an F_SPARSE launch, after the drained-queue
+// mask (a render-service session: in its device control block).
 __device__ __forceinline__ uint32_t* sparse_count_of(uint32_t* chunk_ctr) { return chunk_ctr + VR_MAX_QUEUES * kQueueStride + 2u; }
+__device__ __forceinline__ uint32_t* sparse_count(const RenderParams& p)
+{
+    return p.svc_dev ? &p.svc_dev->sparse_n : sparse_count_of(p.chunk_ctr);
+}
 __device__ __forceinline__ void store_path(const RenderParams& p, uint32_t q, uint32_t slot, const vr4& out, float depth)
 {
     p.paths[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
@@ -1272,12 +1277,19 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
                 Ray r0 = cam;
                 vr4 miss_r;
                 (void)bounce_step<CNT, FEAT>(p, r0, hr, ps, miss_r, cnt);
-                p.paths[slot] = vr3{ miss_r.x, miss_r.y, miss_r.z };
-                p.path_w[slot] = kSharedMissW;
+                if (p.svc_dev) {
+                    // a render-service session: the result serves every launch
+                    // of the session, kept in the pixel's primary record
+                    // (svc_finish_kernel reads it there)
+                    dst[1] = mk4(0.f, miss_r.x, miss_r.y, miss_r.z);
+                } else {
+                    p.paths[slot] = vr3{ miss_r.x, miss_r.y, miss_r.z };
+                    p.path_w[slot] = kSharedMissW;
+                }
                 if (CNT) cnt.shared_miss += 2u * p.n_frames;
             }
             if (__ballot(hit) != 0ull && lane == 0) {
-                const uint32_t at = atomicAdd(sparse_count_of(p.chunk_ctr), 1u);
+                const uint32_t at = atomicAdd(sparse_count(p), 1u);
                 p.sparse_subs[at] = slot >> 6;
             }
         }
@@ -1571,7 +1583,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     const uint32_t n_paths = 2u * p.n_frames;
     constexpr bool SPARSE = (FEAT & F_SPARSE) != 0u;       // the listed sub-tiles only
     // 8x8 sub-tiles of the rank's tiles, or the F_SPARSE list of those holding a hit
-    const uint32_t n_sub = SPARSE ? __builtin_amdgcn_readfirstlane(*sparse_count_of(p.chunk_ctr)) : p.path_stride >> 6;
+    const uint32_t n_sub = SPARSE ? __builtin_amdgcn_readfirstlane(*sparse_count(p)) : p.path_stride >> 6;
     constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;      // instrumented copy (vrhip_render_profiled)
     Cnt cnt;
 
@@ -1874,7 +1886,9 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
 #if VR_X != 1
     if (blockIdx.x == 0u && (tid >> 6) == BT / 64 - 1) { svc_ring_wave(p, lane); return; }
 #endif
-    const uint32_t n_sub = p.path_stride >> 6;             // 8x8 sub-tiles of the rank's tiles
+    constexpr bool SPARSE = (FEAT & F_SPARSE) != 0u;       // the session's listed sub-tiles only
+    // 8x8 sub-tiles of the rank's tiles, or those the session's primary pass listed
+    const uint32_t n_sub = SPARSE ? __builtin_amdgcn_readfirstlane(*sparse_count(p)) : p.path_stride >> 6;
     Cnt cnt;
     const uint32_t Q = p.n_queues;
     const uint32_t q0 = blockIdx.x & (Q - 1u);
@@ -1933,7 +1947,8 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
                     seed[rec][0] = svc_ld(&p.svc_dev->desc[sL].first_frame) + (pth >> 1);
                     seed[rec][1] = svc_ld(&p.svc_dev->desc[sL].times[pth >> 1]);
                 }
-                sub = sb; path = pth; lc = sL;
+                sub = SPARSE ? __builtin_amdgcn_readfirstlane(p.sparse_subs[sb]) : sb;
+                path = pth; lc = sL;
                 return GOT;
             }
             // queue qj of launch sL is drained: the drained-queue mask of the
@@ -1984,6 +1999,9 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
         const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
         hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
         hr.bv = b.x;
+        if constexpr (SPARSE) {                            // an escaped pixel: the session's shared result
+            if (hr.kind == HK_NONE) { state = LS_DONE; return; }
+        }
         if constexpr (prim_has_dir<FEAT>()) {
             hr.su = hr.sv = 0.f;
             ray.o = cam_origin(p);
@@ -2045,6 +2063,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
                 state = LS_SETUP;
             }
         }
+        if constexpr (SPARSE) ended = ended || (state == LS_DONE && cur_sub != ~0u);   // escaped items: refill
         const unsigned long long em = __ballot(ended);
         if (em != 0ull) {
             const uint32_t need = (uint32_t)__popcll(em);
@@ -2062,7 +2081,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
             if (next + need > 64u) { cur_sub = nsub; cur_q = nq; cur_L = nL; cslot ^= 1u; next = next + need - 64u; }
             else next += need;
         }
-        if (__ballot(state != LS_DONE) == 0ull) {
+        if (__ballot(state != LS_DONE) == 0ull && (!SPARSE || cur_sub == ~0u)) {
             if (ring == DONE || !wait_chunk()) break;
             next = 64u;
             start(cur_sub, cur_q, cur_L, (uint32_t)lane, cslot);
@@ -2192,6 +2211,12 @@ inline void launch_service_wave(const RenderParams& p, hipStream_t s)
     // the session's camera-ray hits (camera, scene and tiling are fixed for it)
     hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(p.path_stride / kBlockThreads), dim3(kBlockThreads), 0, s, p);
     const uint32_t per_cu = (uint32_t)(4 * svc_waves(STACK, C) * 64 / BT);
+    if constexpr (sparse_ok<FEAT>()) {
+        if (p.sparse_subs) {                      // the listed sub-tiles only
+            hipLaunchKernelGGL((render_service_kernel<STACK, F | F_SPARSE, BT>), dim3(p.wave_blocks * per_cu), dim3(BT), 0, s, p);
+            return;
+        }
+    }
     hipLaunchKernelGGL((render_service_kernel<STACK, F, BT>), dim3(p.wave_blocks * per_cu), dim3(BT), 0, s, p);
 }
 

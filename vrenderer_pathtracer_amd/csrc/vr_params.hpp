@@ -108,7 +108,8 @@ constexpr uint32_t kSvcClosed = 0x80000000u;
 struct SvcDevCtl {                                 // device memory, zeroed when a session opens
     uint32_t ctl;                                  // mirror of the host ring: posted | closed (kSvcClosed), only grows
     uint32_t pad0[31];
-    uint32_t pad1[32];
+    uint32_t sparse_n;                             // F_SPARSE sessions: sub-tiles listed by the primary pass
+    uint32_t pad1[31];
     SvcLaunch desc[kSvcMaxLaunches];               // device copies of the descriptors (sc1 stores, then ctl)
 };
 // per launch: work-queue heads and drained-queue mask, kQueueStride words apart

@@ -162,6 +162,7 @@ struct vrhip_ctx {
         uint32_t* qctl = nullptr; size_t qctl_slots = 0;    // work-queue heads per launch slot
         uint8_t* scratch = nullptr; size_t scratch_cap = 0; // launch slots' path results
         vr4* prim = nullptr; size_t prim_cap = 0;           // the session's primary records, 2 float4 per owned pixel
+        uint32_t* subs = nullptr; size_t subs_cap = 0;      // F_SPARSE sessions: the sub-tiles holding a hit
         uint8_t* staging = nullptr; size_t staging_cap = 0; // deferred gathers: per launch slot
         uint32_t slots = 0, kmax = 0, posted = 0;
         size_t slot_bytes = 0;
@@ -1009,8 +1010,8 @@ static void svc_free(vrhip_ctx* c)
         S.ring_used[i] = false;
     }
     S.host = nullptr;
-    dfree(S.dev); dfree(S.qctl); dfree(S.scratch); dfree(S.prim); dfree(S.staging);
-    S.qctl_slots = S.scratch_cap = S.prim_cap = S.staging_cap = 0;
+    dfree(S.dev); dfree(S.qctl); dfree(S.scratch); dfree(S.prim); dfree(S.staging); dfree(S.subs);
+    S.qctl_slots = S.scratch_cap = S.prim_cap = S.staging_cap = S.subs_cap = 0;
     if (S.k0) (void)hipEventDestroy(S.k0);
     if (S.k1) (void)hipEventDestroy(S.k1);
     if (S.finished) (void)hipEventDestroy(S.finished);
@@ -1123,6 +1124,9 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     if ((rc = grow(S.prim, S.prim_cap, 32u * stride)) != VRHIP_OK) return rc;
     if ((rc = grow(S.staging, S.staging_cap, (size_t)slots * stage_bytes)) != VRHIP_OK) return rc;
     if ((rc = grow(S.qctl, S.qctl_slots, (size_t)slots * vr::kSvcQctlWords * 4u)) != VRHIP_OK) return rc;
+    // HDRI scenes: escaped camera rays' pixels leave the session's paths (F_SPARSE)
+    const bool sparse = VR_SPARSE_HDRI != 0 && !c->cornell && (p.flags & vr::F_STRICT) == 0u;
+    if (sparse && (rc = grow(S.subs, S.subs_cap, 4u * (stride / 64u))) != VRHIP_OK) return rc;
     if (!S.k0 && (rc = take_event(c, &S.k0)) != VRHIP_OK) return rc;
     if (!S.k1 && (rc = take_event(c, &S.k1)) != VRHIP_OK) return rc;
     S.slot_bytes = slot_bytes; S.slots = slots; S.kmax = kmax; S.posted = 0;
@@ -1130,6 +1134,7 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     S.p = p;
     S.p.paths = reinterpret_cast<vr3*>(S.scratch);
     S.p.prim = S.prim;
+    S.p.sparse_subs = sparse ? S.subs : nullptr;
     S.host = S.rings[ri];
     S.p.svc_host = S.rings_dev[ri]; S.p.svc_dev = S.dev; S.p.svc_qctl = S.qctl;
     S.p.svc_slot_bytes = slot_bytes; S.p.svc_kmax = kmax;
