@@ -15,7 +15,7 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     if (tile == 0 && tid <= VR_MAX_QUEUES && p.chunk_ctr) p.chunk_ctr[tid * kQueueStride] = 0u;
     if (tile == 0 && tid == VR_MAX_QUEUES && p.chunk_ctr) {
         p.chunk_ctr[tid * kQueueStride + 1u] = 0u;      // drained-queue mask
-        *sparse_count_of(p.chunk_ctr) = 0u;            // an F_SPARSE launch's sub-tile list
+        *sparse_count_of(p.chunk_ctr) = 0u;            // an F_SPARSE launch's pixel list
     }
     const int wave = (int)tid >> 6, lane = (int)tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(kBlockThreads) svc_finish_kernel(const RenderP
     float last_w = 0.f;
     // an F_SPARSE session's escaped pixel: its one result for every path of
     // every launch, in its primary record (primary_kernel), depth term 1
-    const bool shared = p.sparse_subs && __float_as_int(p.prim[2u * slot].y) == (int)HK_NONE;
+    const bool shared = p.sparse_px && __float_as_int(p.prim[2u * slot].y) == (int)HK_NONE;
     vr4 shared_h = mk4(0.f, 0.f, 0.f, 0.f);
     if (shared) {
         const vr4 b = p.prim[2u * slot + 1u];

@@ -1021,7 +1021,7 @@ __device__ __forceinline__ bool escaped(float x) { return __float_as_uint(x) == 
 // depth term of -1 (a real one is >= 0); the other groups store nothing and
 // finish_kernel adds that one result for every path, in path order.
 constexpr float kSharedMissW = -1.0f;
-// The listed sub-tile count of an F_SPARSE launch, after the drained-queue
+// The listed pixel count of an F_SPARSE launch, after the drained-queue
 // mask (a render-service session: in its device control block).
 __device__ __forceinline__ uint32_t* sparse_count_of(uint32_t* chunk_ctr) { return chunk_ctr + VR_MAX_QUEUES * kQueueStride + 2u; }
 __device__ __forceinline__ uint32_t* sparse_count(const RenderParams& p)
@@ -1265,11 +1265,12 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
     else
         dst[1] = mk4(hr.bv, hr.su, hr.sv, 0.f);
     if constexpr (sparse_ok<FEAT>()) {
-        if (p.sparse_subs) {
+        if (p.sparse_px) {
             // F_SPARSE launch: an escaped camera ray gives every path of the
             // pixel the same result (render_kernel's shared escape), stored
-            // once; the sub-tile joins the path kernel's list if any of its
-            // pixels hit the scene
+            // once; the pixels that hit the scene join the path kernel's list
+            // (one atomic per wave, the wave's hits contiguous: an 8x8
+            // sub-tile's pixels stay together in the path kernel's chunks)
             if (!hit) {
                 PathState ps;
                 uint32_t d0 = 0, d1 = 0;                   // the miss branch draws no random number
@@ -1288,9 +1289,13 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
                 }
                 if (CNT) cnt.shared_miss += 2u * p.n_frames;
             }
-            if (__ballot(hit) != 0ull && lane == 0) {
-                const uint32_t at = atomicAdd(sparse_count(p), 1u);
-                p.sparse_subs[at] = slot >> 6;
+            const unsigned long long hm = __ballot(hit);
+            if (hm != 0ull) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(sparse_count(p), (uint32_t)__popcll(hm));
+                base = (uint32_t)__shfl((int)base, 0, 64);
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+                if (hit) p.sparse_px[base + r] = slot;
             }
         }
     }
@@ -1581,9 +1586,12 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
     const uint32_t n_paths = 2u * p.n_frames;
-    constexpr bool SPARSE = (FEAT & F_SPARSE) != 0u;       // the listed sub-tiles only
-    // 8x8 sub-tiles of the rank's tiles, or the F_SPARSE list of those holding a hit
-    const uint32_t n_sub = SPARSE ? __builtin_amdgcn_readfirstlane(*sparse_count(p)) : p.path_stride >> 6;
+    constexpr bool SPARSE = (FEAT & F_SPARSE) != 0u;       // the listed pixels only
+    // chunk rows: the 8x8 sub-tiles of the rank's tiles, or (F_SPARSE) runs
+    // of 64 listed pixels -- the last run padded with the last pixel, whose
+    // paths then run twice and store the same bits to the same slots
+    const uint32_t n_px = SPARSE ? __builtin_amdgcn_readfirstlane(*sparse_count(p)) : 0u;
+    const uint32_t n_sub = SPARSE ? (n_px + 63u) >> 6 : p.path_stride >> 6;
     constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;      // instrumented copy (vrhip_render_profiled)
     Cnt cnt;
 
@@ -1611,10 +1619,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             if (lane == 0) v = atomicAdd(p.chunk_ctr + qj * kQueueStride, 1u);
             const uint32_t sb = queue_item(qj, __builtin_amdgcn_readfirstlane(v), Q, n_paths, path);
             if (sb < n_sub) {
-                if constexpr (SPARSE) {                    // the listed sub-tile
-                    sub = __builtin_amdgcn_readfirstlane(p.sparse_subs[sb]);
-                    return;
-                }
+                if constexpr (SPARSE) { sub = sb; return; }   // a run of listed pixels
 #if VR_XCD_BANDS
                 // longest-first: the XCD's sub-tiles in the order of the
                 // previous launch's cost (order_kernel); else band order
@@ -1686,9 +1691,13 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         if (sub == ~0u) { state = LS_DONE; return; }
         q = path;
         slot = sub * 64u + px;
+        if constexpr (SPARSE) {                            // the listed pixel
+            const uint32_t k = slot < n_px ? slot : n_px - 1u;
+            slot = p.sparse_px[k];
+        }
         const uint32_t f = q >> 1;
         uint32_t x, y;
-        sub_pixel(p, sub, px, x, y);
+        sub_pixel(p, slot >> 6, slot & 63u, x, y);
         uint32_t s1 = x * (p.first_frame + f);
         uint32_t s2 = y * p.times[f];
         if (q & 1u) (void)hash_seeds(s1, s2);              // the frame's second sample
@@ -1704,11 +1713,6 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
         hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
         hr.bv = b.x;
-        if constexpr (SPARSE) {
-            // an escaped pixel of a listed sub-tile: its shared result is
-            // stored (primary_kernel); the lane takes the next item
-            if (hr.kind == HK_NONE) { state = LS_DONE; return; }
-        }
         if constexpr (prim_has_dir<FEAT>()) {
             hr.su = hr.sv = 0.f;
             ray.o = cam_origin(p);
@@ -1787,8 +1791,6 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 state = LS_SETUP;
             }
         }
-        // (F_SPARSE: lanes whose item was an escaped pixel take another)
-        if constexpr (SPARSE) ended = ended || (state == LS_DONE && cur_sub != ~0u);
         const unsigned long long em = __ballot(ended);
         if (em != 0ull) {
             const uint32_t need = (uint32_t)__popcll(em);
@@ -1803,7 +1805,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             if (next + need > 64u) { cur_sub = nsub; cur_q = nq; next = next + need - 64u; }
             else next += need;
         }
-        if (__ballot(state != LS_DONE) == 0ull && (!SPARSE || cur_sub == ~0u)) break;
+        if (__ballot(state != LS_DONE) == 0ull) break;
     }
     if (CNT) flush_counts(p, cnt, lane, true);
 }
@@ -1886,9 +1888,11 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
 #if VR_X != 1
     if (blockIdx.x == 0u && (tid >> 6) == BT / 64 - 1) { svc_ring_wave(p, lane); return; }
 #endif
-    constexpr bool SPARSE = (FEAT & F_SPARSE) != 0u;       // the session's listed sub-tiles only
-    // 8x8 sub-tiles of the rank's tiles, or those the session's primary pass listed
-    const uint32_t n_sub = SPARSE ? __builtin_amdgcn_readfirstlane(*sparse_count(p)) : p.path_stride >> 6;
+    constexpr bool SPARSE = (FEAT & F_SPARSE) != 0u;       // the session's listed pixels only
+    // chunk rows: 8x8 sub-tiles, or (F_SPARSE) runs of 64 pixels the
+    // session's primary pass listed (the last run padded, render_wave_kernel)
+    const uint32_t n_px = SPARSE ? __builtin_amdgcn_readfirstlane(*sparse_count(p)) : 0u;
+    const uint32_t n_sub = SPARSE ? (n_px + 63u) >> 6 : p.path_stride >> 6;
     Cnt cnt;
     const uint32_t Q = p.n_queues;
     const uint32_t q0 = blockIdx.x & (Q - 1u);
@@ -1947,8 +1951,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
                     seed[rec][0] = svc_ld(&p.svc_dev->desc[sL].first_frame) + (pth >> 1);
                     seed[rec][1] = svc_ld(&p.svc_dev->desc[sL].times[pth >> 1]);
                 }
-                sub = SPARSE ? __builtin_amdgcn_readfirstlane(p.sparse_subs[sb]) : sb;
-                path = pth; lc = sL;
+                sub = sb; path = pth; lc = sL;
                 return GOT;
             }
             // queue qj of launch sL is drained: the drained-queue mask of the
@@ -1990,8 +1993,12 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
         if (sub == ~0u) { state = LS_DONE; return; }       // render's per-sample prologue (:817-844)
         q = path | (lc << 8);
         slot = sub * 64u + px;
+        if constexpr (SPARSE) {                            // the listed pixel
+            const uint32_t k = slot < n_px ? slot : n_px - 1u;
+            slot = p.sparse_px[k];
+        }
         uint32_t x, y;
-        sub_pixel(p, sub, px, x, y);
+        sub_pixel(p, slot >> 6, slot & 63u, x, y);
         uint32_t s1 = x * seed[rec][0];                    // x * (first frame + frame)
         uint32_t s2 = y * seed[rec][1];
         if (path & 1u) (void)hash_seeds(s1, s2);           // the frame's second sample
@@ -1999,9 +2006,6 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
         const vr4 a = p.prim[2u * slot], b = p.prim[2u * slot + 1u];
         hr.t = a.x; hr.kind = __float_as_int(a.y); hr.idx = __float_as_int(a.z); hr.bu = a.w;
         hr.bv = b.x;
-        if constexpr (SPARSE) {                            // an escaped pixel: the session's shared result
-            if (hr.kind == HK_NONE) { state = LS_DONE; return; }
-        }
         if constexpr (prim_has_dir<FEAT>()) {
             hr.su = hr.sv = 0.f;
             ray.o = cam_origin(p);
@@ -2063,7 +2067,6 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
                 state = LS_SETUP;
             }
         }
-        if constexpr (SPARSE) ended = ended || (state == LS_DONE && cur_sub != ~0u);   // escaped items: refill
         const unsigned long long em = __ballot(ended);
         if (em != 0ull) {
             const uint32_t need = (uint32_t)__popcll(em);
@@ -2081,7 +2084,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
             if (next + need > 64u) { cur_sub = nsub; cur_q = nq; cur_L = nL; cslot ^= 1u; next = next + need - 64u; }
             else next += need;
         }
-        if (__ballot(state != LS_DONE) == 0ull && (!SPARSE || cur_sub == ~0u)) {
+        if (__ballot(state != LS_DONE) == 0ull) {
             if (ring == DONE || !wait_chunk()) break;
             next = 64u;
             start(cur_sub, cur_q, cur_L, (uint32_t)lane, cslot);
@@ -2177,7 +2180,7 @@ inline void launch_wave(const RenderParams& p, uint32_t n_tiles, hipStream_t s)
         return capped < 1u ? 1u : (capped < full ? capped : full);
     };
     if constexpr (sparse_ok<FEAT>()) {
-        if (p.sparse_subs) {                      // the listed sub-tiles only (same shape and residency)
+        if (p.sparse_px) {                        // the listed pixels only (same shape and residency)
             const int bt = (B == 0 && p.small_blocks) ? BTS : BT;
             if (bt == BTS)
                 hipLaunchKernelGGL((render_wave_kernel<STACK, FEAT | F_SPARSE, BTS>), dim3(p.wave_blocks * per_cu(BTS)),
@@ -2212,7 +2215,7 @@ inline void launch_service_wave(const RenderParams& p, hipStream_t s)
     hipLaunchKernelGGL((primary_kernel<STACK, FEAT>), dim3(p.path_stride / kBlockThreads), dim3(kBlockThreads), 0, s, p);
     const uint32_t per_cu = (uint32_t)(4 * svc_waves(STACK, C) * 64 / BT);
     if constexpr (sparse_ok<FEAT>()) {
-        if (p.sparse_subs) {                      // the listed sub-tiles only
+        if (p.sparse_px) {                        // the listed pixels only
             hipLaunchKernelGGL((render_service_kernel<STACK, F | F_SPARSE, BT>), dim3(p.wave_blocks * per_cu), dim3(BT), 0, s, p);
             return;
         }

@@ -42,10 +42,9 @@ enum Flags : uint32_t {
     // primary records, results per launch slot (vrhip_api.cpp Session)
     F_SERVICE = 1u << 15,
     // compile-time only: the path kernel of HDRI mesh launches that skip the
-    // pixels whose camera ray escapes (RenderParams::sparse_subs): the
-    // primary pass stores each such pixel's one shared result and lists the
-    // 8x8 sub-tiles holding a camera-ray hit; the path kernel runs the paths
-    // of the listed sub-tiles only
+    // pixels whose camera ray escapes (RenderParams::sparse_px): the primary
+    // pass stores each such pixel's one shared result and lists the pixels
+    // whose camera ray hits the scene; the path kernel runs their paths only
     F_SPARSE = 1u << 16,
 };
 constexpr int kMaxFramesPerLaunch = 64;
@@ -108,7 +107,7 @@ constexpr uint32_t kSvcClosed = 0x80000000u;
 struct SvcDevCtl {                                 // device memory, zeroed when a session opens
     uint32_t ctl;                                  // mirror of the host ring: posted | closed (kSvcClosed), only grows
     uint32_t pad0[31];
-    uint32_t sparse_n;                             // F_SPARSE sessions: sub-tiles listed by the primary pass
+    uint32_t sparse_n;                             // F_SPARSE sessions: pixels listed by the primary pass
     uint32_t pad1[31];
     SvcLaunch desc[kSvcMaxLaunches];               // device copies of the descriptors (sc1 stores, then ctl)
 };
@@ -189,10 +188,11 @@ struct RenderParams {
     size_t svc_slot_bytes;           // result scratch per launch slot: 2 svc_kmax rows of path_stride vr3, then path_w
     uint32_t svc_kmax;               // frames per launch a slot holds
     uint32_t svc_idle_ticks;         // 100 MHz ticks with no new launch after which the service retires
-    // F_SPARSE launches (nullptr otherwise): the sub-tiles holding a
-    // camera-ray hit, appended by primary_kernel (their count at
-    // sparse_count_of(chunk_ctr), reset by finish_kernel)
-    uint32_t* sparse_subs;
+    // F_SPARSE launches (nullptr otherwise): the slots of the owned pixels
+    // whose camera ray hits the scene, appended by primary_kernel one wave
+    // (8x8 sub-tile) at a time (their count at sparse_count(p), reset by
+    // finish_kernel / zeroed when a session opens)
+    uint32_t* sparse_px;
     uint32_t times[kMaxFramesPerLaunch];
 };
 

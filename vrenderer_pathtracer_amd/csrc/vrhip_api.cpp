@@ -113,6 +113,8 @@ struct vrhip_ctx {
         uint32_t* sub_order = nullptr;
         size_t sub_cap = 0;          // sub-tiles the buffers hold
         uint32_t order_nsub = 0;     // sub-tile count the order was sorted for (0: none)
+        uint32_t* px_list = nullptr;     // F_SPARSE launches: the pixels whose camera ray hits (RenderParams::sparse_px)
+        size_t px_cap = 0;
         hipEvent_t done = nullptr;   // recorded on `s` after the render kernels
         hipEvent_t finished = nullptr;   // recorded on `stream` after the finish pass that read this scratch
         hipEvent_t ordered = nullptr;    // recorded on `s` after the order pass sorting this scratch's costs
@@ -162,7 +164,7 @@ struct vrhip_ctx {
         uint32_t* qctl = nullptr; size_t qctl_slots = 0;    // work-queue heads per launch slot
         uint8_t* scratch = nullptr; size_t scratch_cap = 0; // launch slots' path results
         vr4* prim = nullptr; size_t prim_cap = 0;           // the session's primary records, 2 float4 per owned pixel
-        uint32_t* subs = nullptr; size_t subs_cap = 0;      // F_SPARSE sessions: the sub-tiles holding a hit
+        uint32_t* subs = nullptr; size_t subs_cap = 0;      // F_SPARSE sessions: the pixels whose camera ray hits
         uint8_t* staging = nullptr; size_t staging_cap = 0; // deferred gathers: per launch slot
         uint32_t slots = 0, kmax = 0, posted = 0;
         size_t slot_bytes = 0;
@@ -594,7 +596,7 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->comm) (void)ncclCommDestroy(c->comm);
     dfree(c->comm_send); dfree(c->comm_recv);
     for (auto& l : c->lane) {
-        dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr); dfree(l.sub_cost); dfree(l.sub_order);
+        dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr); dfree(l.sub_cost); dfree(l.sub_order); dfree(l.px_list);
         if (l.done) (void)hipEventDestroy(l.done);
         if (l.ordered) (void)hipEventDestroy(l.ordered);
         if (l.finished) (void)hipEventDestroy(l.finished);
@@ -958,6 +960,12 @@ static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t p
         l.prim_cap = prim_need;
     }
     const size_t n_sub = path_stride / 64u;
+    if (path_stride > l.px_cap) {                         // the F_SPARSE pixel list: one word per owned pixel
+        dfree(l.px_list);
+        l.px_cap = 0;
+        HIP_TRY(hipMalloc((void**)&l.px_list, (size_t)path_stride * sizeof(uint32_t)));
+        l.px_cap = path_stride;
+    }
     if (n_sub > l.sub_cap) {                              // the order buffers hold 8 XCD lists of order_cap(n_sub)
         dfree(l.sub_cost); dfree(l.sub_order);
         l.sub_cap = 0; l.order_nsub = 0;
@@ -1126,7 +1134,7 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     if ((rc = grow(S.qctl, S.qctl_slots, (size_t)slots * vr::kSvcQctlWords * 4u)) != VRHIP_OK) return rc;
     // HDRI scenes: escaped camera rays' pixels leave the session's paths (F_SPARSE)
     const bool sparse = VR_SPARSE_HDRI != 0 && !c->cornell && (p.flags & vr::F_STRICT) == 0u;
-    if (sparse && (rc = grow(S.subs, S.subs_cap, 4u * (stride / 64u))) != VRHIP_OK) return rc;
+    if (sparse && (rc = grow(S.subs, S.subs_cap, 4u * stride)) != VRHIP_OK) return rc;
     if (!S.k0 && (rc = take_event(c, &S.k0)) != VRHIP_OK) return rc;
     if (!S.k1 && (rc = take_event(c, &S.k1)) != VRHIP_OK) return rc;
     S.slot_bytes = slot_bytes; S.slots = slots; S.kmax = kmax; S.posted = 0;
@@ -1134,7 +1142,7 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     S.p = p;
     S.p.paths = reinterpret_cast<vr3*>(S.scratch);
     S.p.prim = S.prim;
-    S.p.sparse_subs = sparse ? S.subs : nullptr;
+    S.p.sparse_px = sparse ? S.subs : nullptr;
     S.host = S.rings[ri];
     S.p.svc_host = S.rings_dev[ri]; S.p.svc_dev = S.dev; S.p.svc_qctl = S.qctl;
     S.p.svc_slot_bytes = slot_bytes; S.p.svc_kmax = kmax;
@@ -1326,7 +1334,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
         // HDRI mesh launches with a primary pass skip the pixels whose camera
         // ray escapes: one shared result each, the path kernel over the
-        // sub-tiles holding a hit (F_SPARSE, vr_kernel.hpp primary_kernel)
+        // pixels whose camera ray hits (F_SPARSE, vr_kernel.hpp primary_kernel)
         const bool sparse = VR_SPARSE_HDRI != 0 && wave_kernel && !c->cornell && count != 1 &&
                             (f & vr::F_STRICT) == 0u && !p.inline_prim;
         p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? (c->cornell ? VR_QUEUES : VR_QUEUES_HDRI)
@@ -1361,10 +1369,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             if (ovl) c->parity = (c->parity + 1u) % VR_PATH_STREAMS;
             p.paths = reinterpret_cast<vr::vr3*>(l.paths); p.path_w = reinterpret_cast<float*>(p.paths + need);
             p.prim = l.prim; p.chunk_ctr = l.chunk_ctr;
-            // the F_SPARSE sub-tile list lives in the order buffer, which a
-            // later one-frame launch on this scratch then must not take as an order
-            p.sparse_subs = sparse ? l.sub_order : nullptr;
-            if (sparse) l.order_nsub = 0;
+            p.sparse_px = sparse ? l.px_list : nullptr;
             // longest-first: launches whose drain is a large share of them (one
             // frame per call, shards) measure per sub-tile costs and take their
             // sub-tiles in the order the previous launch on this scratch measured
