@@ -226,6 +226,7 @@ def test_profiled_render_is_the_production_render(native, cfg, w, h, frames):
     r = VRendererHIP(0)
     scenes.load_into(r, sc)
     e = r.render_profiled(frames=frames, times=times)
+    r_kind = r.last_launch_info()["kind"]
     got = r.read_accum(), r.read_rgba8(), r.read_depth8()
     r.set_strict_traversal(True)
     r.clearBuffer()
@@ -236,8 +237,11 @@ def test_profiled_render_is_the_production_render(native, cfg, w, h, frames):
     assert e["node_visits_lds"] <= e["node_visits"] <= ref["node_visits"]
     assert e["tri_tests"] <= ref["tri_tests"] and e["tri_loads"] >= e["tri_tests"]
     assert e["nmap_hits"] <= e["mesh_hits"]
-    # escaped camera rays of sphere-only HDRI scenes are fetched once per pixel (shared_miss_paths)
-    assert e["hdr_fetches"] <= ref["hdr_fetches"] and e["brdf_fetches"] <= ref["brdf_fetches"]
+    # escaped camera rays of HDRI scenes are fetched once per pixel (shared_miss_paths); the
+    # path pool over listed pixels (F_SPARSE) pads its last chunk of each path index with
+    # the last listed pixel, whose duplicate paths (< 64 per path index) are counted too
+    pad = 63 * 2 * frames if r_kind == "path_pool" else 0
+    assert e["hdr_fetches"] <= ref["hdr_fetches"] + 4 * pad and e["brdf_fetches"] <= ref["brdf_fetches"] + 4 * pad
     assert e["hdr_fetches"] + e["shared_miss_paths"] >= ref["hdr_fetches"]
     if sc.get("mesh_flat") is None:
         assert e["node_visits"] == 0 and e["mesh_hits"] == 0

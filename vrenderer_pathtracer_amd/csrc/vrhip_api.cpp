@@ -1392,7 +1392,10 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             c->kev_pending.push_back({ k0, k1, 1u });
             HIP_TRY(hipEventRecord(k0, rs));
         }
-        if (count == 0) { c->last_split = p.split; c->last_use_scratch = p.use_scratch; c->last_kind = wave_kernel ? 1u : 0u; }
+        if (count != 1) {                 // production and its instrumented copy (same shape)
+            c->last_split = p.split; c->last_use_scratch = p.use_scratch;
+            c->last_kind = wave_kernel ? 1u : 0u;
+        }
         int e = vr::launch_render(p, n_tiles, stack, count, rs);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
         if (n_tiles) HIP_TRY(hipEventRecord(k1, rs));
