@@ -118,3 +118,24 @@ def test_feature_class_launch_kinds_bitexact(native, oracle, name, mode):
             own[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16] = True
         assert (ga[own].view(np.uint32) == oa[own].view(np.uint32)).all()
         assert not ga[~own].any()
+
+
+@pytest.mark.parametrize("view,service", [("away", None), ("away", 1), ("close", None)])
+def test_escaped_ray_skipping_extremes_bitexact(native, oracle, view, service):
+    """HDRI mesh launches skip the pixels whose camera ray escapes (F_SPARSE):
+    with the camera turned away from the knot no pixel is listed (the path
+    kernel gets no work, every pixel takes its shared result), close to the
+    knot nearly every pixel is; both, in launches and in a render-service
+    session, equal the oracle bit for bit."""
+    sc = scenes.make_scene("C3", 96, 64)
+    if view == "away":        # looking down +z, away from the knot at the origin
+        sc["camera"] = dict(sc["camera"], dir=(0.0, 0.0, 1.0), right=(-1.0, 0.0, 0.0))
+    else:                     # 30 units from the knot's centre
+        sc["camera"] = dict(sc["camera"], origin=(0.0, 0.0, 30.0))
+    times = [4321 + 3 * i for i in range(5)]
+    ga, gr, gd, nf = run(sc, times, one_frame=service is not None, service=service)
+    oa, orgba, od, _ = po.render(sc, frames=len(times), times=times, libm=po.LIBM_PORTABLE)
+    assert nf == len(times)
+    bitexact(ga, oa, sc, f"{view} accum")
+    bitexact(gr, orgba, sc, f"{view} rgba8")
+    bitexact(gd, od, sc, f"{view} depth8")
