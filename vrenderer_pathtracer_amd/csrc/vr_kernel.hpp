@@ -495,8 +495,15 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 // the HDRI scenes lose at 10 (C3 -1.3 %, C5 -1.2 %) and keep VR_NODE_BREAK
 #define VR_NODE_BREAK_CORNELL 10
 #endif
+// Kernels over the listed pixels of HDRI scenes (F_SPARSE: every lane's path
+// hit the mesh at its camera ray): 8 (r04, against 6: C3 +0.7 %, C5 +0.7 %,
+// C3D +1.3 %; 10: -1.5 / +0.4 / +0.7 %)
+#ifndef VR_NODE_BREAK_SPARSE
+#define VR_NODE_BREAK_SPARSE 8
+#endif
 template <uint32_t FEAT>
 constexpr int node_break() {
+    if ((FEAT & F_SPARSE) != 0u) return VR_NODE_BREAK_SPARSE;
     // one-frame kernels (F_INLINE_PRIM) keep 6: the interactive C2 rate fell
     // 2,147 -> 2,103 Mpaths/s with 10 (r02h)
     return ((FEAT & (F_EXACT | F_CLASS)) && (FEAT & F_CORNELL) && !(FEAT & F_INLINE_PRIM)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK;
