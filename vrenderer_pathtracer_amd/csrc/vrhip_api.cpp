@@ -1337,8 +1337,11 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // pixels whose camera ray hits (F_SPARSE, vr_kernel.hpp primary_kernel)
         const bool sparse = VR_SPARSE_HDRI != 0 && wave_kernel && !c->cornell && count != 1 &&
                             (f & vr::F_STRICT) == 0u && !p.inline_prim;
-        p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25) ? (c->cornell ? VR_QUEUES : VR_QUEUES_HDRI)
-                                                                        : VR_QUEUES_LARGE;
+        // (launches over the listed pixels of HDRI scenes -- a fifth of the
+        // paths, all of them mesh paths -- take VR_QUEUES like the Cornell
+        // box: C3 16 / 32 / 64 heads 16,630 / 16,408 / 16,172 Mpaths/s, r04)
+        p.n_queues = (size_t)p.path_stride * 2u * k < ((size_t)1 << 25)
+                         ? ((c->cornell || sparse) ? VR_QUEUES : VR_QUEUES_HDRI) : VR_QUEUES_LARGE;
         // VRHIP_QUEUES: work-queue heads for experiments (a power of two, 8..VR_MAX_QUEUES)
         static const uint32_t env_queues = [] {
             const char* e = std::getenv("VRHIP_QUEUES");
