@@ -59,6 +59,29 @@ def timed_durations(trace_csv):
     return out
 
 
+def timed_busy_ms(trace_csv):
+    """Busy time per launch: the union of the timed production dispatches'
+    intervals / STEPS.  Equals the sum of the averages when launches run one
+    after another; with launches overlapped on several path streams (C1, C4:
+    per-dispatch durations stretch while they share the GPU) it is the figure
+    bench.py's events measure."""
+    per = defaultdict(list)
+    for r in csv.DictReader(open(trace_csv)):
+        k = production(r["Kernel_Name"])
+        if k:
+            per[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    iv = sorted(x for v in per.values() for x in sorted(v)[-STEPS:])
+    busy, end = 0, None
+    for a, b in iv:
+        if end is None or a > end:
+            busy += b - a
+            end = b
+        elif b > end:
+            busy += b - end
+            end = b
+    return busy / STEPS / 1e6
+
+
 def timed_counter(pmc_csv, counter):
     per = defaultdict(list)
     for r in csv.DictReader(open(pmc_csv)):
@@ -110,7 +133,11 @@ def main():
         md.append(f"\n## {cfg}\n\n| kernel | dispatches | avg ms (timed) |\n|---|---|---|\n")
         for (k, full), (ms, n) in sorted(dur.items()):
             md.append(f"| `{full.replace('void ', '').split('(')[0]}` | {n} | {ms:.4f} |\n")
+        busy_ms = timed_busy_ms(traces[0])
         md.append(f"\nRender launch (sum of the production kernels) = **{launch_ms:.4f} ms** per launch")
+        if abs(busy_ms - launch_ms) > 0.02 * launch_ms:
+            md.append(f" (dispatches overlapped on several path streams: busy time "
+                      f"{busy_ms:.4f} ms per launch, the union of the timed dispatches' intervals / {STEPS})")
         if traced_bench:
             rl = traced_bench["roofline"]
             md.append(f"; bench.py's HIP events in the same profiled run: {rl['avg_launch_ms']:.4f} ms "
