@@ -466,11 +466,17 @@ def test_pipelined_steps_with_scene_changes_equal_synchronous(native, cfg, overl
     assert np.array_equal(c_sync, c_pipe)
 
 
-def _random_soup(seed, n, leaf):
+def _random_soup(seed, n, leaf, cluster=1):
+    """n random triangles; with cluster > 1, groups of `cluster` near-copies
+    of one triangle (boxes no split separates: leaves of up to `leaf`)."""
     from vrenderer_pathtracer_amd import build_flat
     rng = np.random.default_rng(seed)
-    c = rng.uniform(-30, 30, (n, 1, 3))
-    P = (c + rng.normal(0, 4, (n, 3, 3))).reshape(-1, 3).astype(np.float32)
+    c = np.repeat(rng.uniform(-30, 30, (n // cluster, 1, 3)), cluster, axis=0)
+    if cluster == 1:
+        P = (c + rng.normal(0, 4, (n, 3, 3))).reshape(-1, 3).astype(np.float32)
+    else:                             # near-copies of one triangle per group
+        base = np.repeat(rng.normal(0, 4, (n // cluster, 3, 3)), cluster, axis=0)
+        P = (c + base + rng.normal(0, 0.05, (n, 3, 3))).reshape(-1, 3).astype(np.float32)
     T = rng.normal(0, 1, (3 * n, 3)).astype(np.float32)
     m = dict(positions=P, normals=(T / np.linalg.norm(T, axis=1, keepdims=True)).astype(np.float32),
              tangents=np.tile([1, 0, 0], (3 * n, 1)).astype(np.float32),
@@ -479,7 +485,7 @@ def _random_soup(seed, n, leaf):
     return build_flat(m, max_leaf_tris=leaf)
 
 
-@pytest.mark.parametrize("cfg,leaf", [("C2", 3), ("C3", 5), ("C2", 1)])
+@pytest.mark.parametrize("cfg,leaf", [("C2", 3), ("C3", 5), ("C2", 1), ("C2", 16), ("C3", 40)])
 def test_random_soup_bitexact_vs_portable_oracle(native, oracle, cfg, leaf):
     """Overlapping random triangles (odd leaf sizes exercise the paired
     triangle loads' tail): strict traversal bit-exact against the oracle, the
@@ -489,7 +495,11 @@ def test_random_soup_bitexact_vs_portable_oracle(native, oracle, cfg, leaf):
     by more than the 2^-10 culling margin through fp32 rounding -- none
     measured)."""
     sc = scenes.make_scene(cfg, 96, 64)
-    sc["mesh_flat"] = _random_soup(11 + leaf, 1500, leaf)
+    sc["mesh_flat"] = _random_soup(11 + leaf, 1500, leaf, cluster=20 if leaf > 8 else 1)
+    if leaf > 8:                      # wide leaves reach the leaf loop's longer runs of pairs
+        v = sc["mesh_flat"]["verts"].view(np.uint32)
+        ends = np.flatnonzero((v[:, 0] == 0x80000000) & (v[:, 1] == 0) & (v[:, 2] == 0))
+        assert int(np.diff(np.concatenate([[-1], ends])).max() - 1) // 3 > 8
     times = [sc["time"], sc["time"] + 1]
     oa, orgba, _, _ = po.render(sc, frames=2, times=times, libm=po.LIBM_PORTABLE)
     sa, srgba, _, _ = gpu_render(sc, 2, times, strict=True)
