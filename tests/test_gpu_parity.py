@@ -687,3 +687,23 @@ def test_longest_first_order_is_scheduling_only(native, oracle, cfg, tiling, ove
     if tiling is None:
         ref, _, _, _ = oracle.render(sc, frames=len(times), times=times, libm=oracle.LIBM_PORTABLE)
         assert_bitexact(acc1, ref, sc, f"{cfg} ordered one-frame calls")
+
+
+@pytest.mark.parametrize("halves", [True, False])
+def test_hdr_storage_bitexact_vs_portable_oracle(native, oracle, halves):
+    """Environment maps whose values are all halves (the reference's
+    Imf::Rgba input, and the procedural map) and float maps that are not
+    (every colour one ulp above a half) both equal the oracle bit for bit.
+    (A half4 device copy of half-valued maps was measured and not kept:
+    DESIGN.md section 4 table.)"""
+    sc = scenes.make_scene("C3", 96, 64)
+    if not halves:
+        h = sc["hdr"].copy()
+        h[..., :3] = np.nextafter(h[..., :3], np.float32(np.inf))
+        assert not np.array_equal(h.astype(np.float16).astype(np.float32), h)
+        sc["hdr"] = h
+    times = [sc["time"], sc["time"] + 1]
+    oa, orgba, _, _ = po.render(sc, frames=2, times=times, libm=po.LIBM_PORTABLE)
+    ga, grgba, _, _ = gpu_render(sc, 2, times)
+    assert_bitexact(ga, oa, sc, "accum")
+    assert_bitexact(grgba, orgba, sc, "rgba8")
