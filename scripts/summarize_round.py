@@ -147,7 +147,7 @@ def main():
             traffic = int((2 * fetch + write) * 1024)
             paths = traced_bench["config"]["paths_per_step"] if traced_bench else None
             json.dump({"hbm_bytes_per_launch": traffic, "fetch_size_kib": fetch, "write_size_kib": write,
-                       "launch_ms_trace": launch_ms, "paths_per_launch": paths,
+                       "launch_ms_trace": launch_ms, "busy_ms_trace": busy_ms, "paths_per_launch": paths,
                        "source": f"profiles/{name}_summary.md ({os.path.basename(src.rstrip('/'))}, fetch_{cfg} / write_{cfg})",
                        "note": "2*FETCH_SIZE + WRITE_SIZE (KiB -> B) per render launch (production render kernels), "
                                f"mean of the {STEPS} timed dispatches; FETCH doubling per MI355X_MICROARCH.md HBM, "
@@ -155,8 +155,8 @@ def main():
                                "(one 128-B line request per line touched, tallied at 64 B)"},
                       open(os.path.join(prof, f"traffic_{cfg.lower()}.json"), "w"), indent=1)
             md.append(f"\nHBM per launch: FETCH_SIZE {fetch / 1024:.1f} MiB, WRITE_SIZE {write / 1024:.1f} MiB -> "
-                      f"2*FETCH + WRITE = {traffic / 1e6:.1f} MB = {traffic / 1e9 / (launch_ms / 1e3):.1f} GB/s "
-                      f"over the launch ({traffic / 1e9 / (launch_ms / 1e3) / 8000:.4f} of 8 TB/s)")
+                      f"2*FETCH + WRITE = {traffic / 1e6:.1f} MB = {traffic / 1e9 / (busy_ms / 1e3):.1f} GB/s "
+                      f"over the launch's busy time ({traffic / 1e9 / (busy_ms / 1e3) / 8000:.4f} of 8 TB/s)")
             if paths:
                 md.append(f"; WRITE_SIZE / (12 B x {paths} path results) = {write * 1024 / (12 * paths):.3f} (12-B radiances since r02e; 16-B float4 before)")
             md.append(".\n")

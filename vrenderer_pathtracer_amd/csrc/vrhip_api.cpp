@@ -1326,9 +1326,13 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // a rank's shard (C5's 8-way shards of 33 M paths: 8-rank projection
         // 0.757 -> 0.78 of linear); whole 720p frames of 29.5 M paths lose
         // with it (C2 -1.7 %, C3 -6 %: two persistent launches contend), as
-        // do C5's 66 M-path 4-way shards (-17 %)
+        // do C5's 66 M-path 4-way shards (-17 %); sphere scenes (render_kernel,
+        // no path pool) overlap up to 2^27 paths: C4's 66 M-path launches
+        // 299 -> 481 G paths/s (r04; C3 -6 %, C5 -14 % forced, so meshes keep
+        // the limit) -- one launch's tail and finish pass run under the next
         const size_t paths_k = (size_t)p.path_stride * 2u * k;
-        const bool ovl_size = paths_k < ((size_t)1 << 24) || (c->nranks > 1 && paths_k < ((size_t)1 << 25));
+        const bool ovl_size = paths_k < ((size_t)1 << 24) || (c->nranks > 1 && paths_k < ((size_t)1 << 25)) ||
+                              (!wave_kernel && paths_k < ((size_t)1 << 27));
         const bool ovl = count == 0 && (c->overlap > 0 || (c->overlap < 0 && ovl_size && in_flight));
         p.small_blocks = small ? 1u : 0u;
         p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
