@@ -31,6 +31,7 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEPS = 5
 RENDER = re.compile(r"vr::(render_wave_kernel|primary_kernel|render_kernel)<([^>]*)>")
+SERVICE = re.compile(r"vr::(render_service_kernel<[^>]*>|svc_finish_kernel)")
 
 
 def production(name):
@@ -80,6 +81,34 @@ def timed_busy_ms(trace_csv):
             busy += b - end
             end = b
     return busy / STEPS / 1e6
+
+
+def service_busy_ms(trace_csv):
+    """Runs whose back-to-back launches went to a render-service session (one
+    persistent render_service_kernel dispatch serving many launches, HDRI mesh
+    scenes): per-dispatch averages do not apply.  Busy time per launch = the
+    union of every production and service dispatch of the run / (STEPS + 1):
+    the warmup launch and the 5 timed ones.  None: no service kernel ran."""
+    iv, svc = [], False
+    for r in csv.DictReader(open(trace_csv)):
+        n = r["Kernel_Name"]
+        if SERVICE.search(n):
+            svc = True
+        elif not production(n):
+            continue
+        iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    if not svc:
+        return None
+    iv.sort()
+    busy, end = 0, None
+    for a, b in iv:
+        if end is None or a > end:
+            busy += b - a
+            end = b
+        elif b > end:
+            busy += b - end
+            end = b
+    return busy / (STEPS + 1) / 1e6
 
 
 def timed_counter(pmc_csv, counter):
@@ -134,8 +163,14 @@ def main():
         for (k, full), (ms, n) in sorted(dur.items()):
             md.append(f"| `{full.replace('void ', '').split('(')[0]}` | {n} | {ms:.4f} |\n")
         busy_ms = timed_busy_ms(traces[0])
+        svc_ms = service_busy_ms(traces[0])
         md.append(f"\nRender launch (sum of the production kernels) = **{launch_ms:.4f} ms** per launch")
-        if abs(busy_ms - launch_ms) > 0.02 * launch_ms:
+        if svc_ms is not None:
+            busy_ms = svc_ms
+            md.append(f" (launches after the first ran in a render-service session, one persistent "
+                      f"dispatch: busy time {svc_ms:.4f} ms per launch, the union of all production and "
+                      f"service dispatches / {STEPS + 1} launches)")
+        elif abs(busy_ms - launch_ms) > 0.02 * launch_ms:
             md.append(f" (dispatches overlapped on several path streams: busy time "
                       f"{busy_ms:.4f} ms per launch, the union of the timed dispatches' intervals / {STEPS})")
         if traced_bench:

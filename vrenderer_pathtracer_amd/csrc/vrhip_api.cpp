@@ -705,6 +705,10 @@ int vrhip_upload_mesh_indexed(vrhip_ctx* c, const float* positions, const float*
                                   (const float*)m.uvs.data(), m.verts.size());
 }
 
+#ifndef VR_SERVICE_HDRI_FRAMES
+#define VR_SERVICE_HDRI_FRAMES 1
+#endif
+
 static int one_upload_hdr(vrhip_ctx* c, const float* rgba, uint32_t w, uint32_t h)
 {
     if (!c || !rgba || w == 0 || h == 0) return fail(VRHIP_ERR_INVALID, "bad hdr arguments");
@@ -1267,8 +1271,13 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         const size_t paths_k = (size_t)p.path_stride * 2u * k_max;
         const bool ovl_size = paths_k < ((size_t)1 << 24) || (c->nranks > 1 && paths_k < ((size_t)1 << 25));
         const bool in_flight = c->svc.open || (c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
+        // HDRI mesh scenes take the service for whole frames too: back-to-back
+        // launches then overlap each other's drain (r04 A/B, 16-frame steps, bit-identical:
+        // C3 16,505 -> 18,948, C5 21,630 -> 22,171 Mpaths/s; the Cornell box's
+        // whole frames lose, C2 4,111 -> 4,021, and keep the shard-size limit)
+        const bool svc_size = ovl_size || (VR_SERVICE_HDRI_FRAMES != 0 && !c->cornell);
         const bool svc = count == 0 && wave_kernel && stack <= 32 && n_tiles > 0 &&
-                         (c->service > 0 || (c->service < 0 && ovl_size && in_flight && c->overlap != 0));
+                         (c->service > 0 || (c->service < 0 && svc_size && in_flight && c->overlap != 0));
         if (!svc) {
             if ((rc = svc_close(c)) != VRHIP_OK) return rc;
         } else {
