@@ -20,11 +20,12 @@ this process starts `torch.distributed.run` with N ranks as a CHILD process
 pixel tiles are dealt round-robin; each rank renders its tiles of every frame,
 then one RCCL gather (ncclGather through the library's C ABI,
 vrhip_comm_gather) brings the RGBA8 tiles to rank 0 per step.  The frame size
-is fixed; a step accumulates 16 x N frames (every GPU renders the equivalent
-of 16 full 1280x720 frames per step and gather, as at N = 1: "weak" scaling
-in samples per step -- SURVEY.md 8e: several frames per gather so that the
-gather and each launch's drain stay small against the step).  --strong keeps
-16 frames per step for any N.
+is fixed and a step accumulates 16 frames whatever N (a fixed display cadence:
+"strong" scaling, the same total work per step).  The line also carries
+`samples_weak`: 16 x N frames per step (every GPU renders the equivalent of 16
+full frames per gather -- SURVEY.md 8e: several frames per gather so that the
+gather and each launch's drain stay small against the step); --weak makes that
+the headline instead.
 
 Prints ONE JSON line (rank 0).  value = total paths of all ranks / max-over-
 ranks wall time of the K timed steps.  "interactive" = the same config one
@@ -210,15 +211,18 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames-per-step", type=int, default=None,
-                    help="frames accumulated per step (= per gather); default 16 x N: every GPU renders 16 "
-                         "full-frame equivalents per step whatever N (weak scaling in samples, fixed resolution)")
-    ap.add_argument("--strong", action="store_true", help="16 frames per step for any N (strong scaling)")
+                    help="frames accumulated per step (= per gather); default 16 whatever N (fixed cadence)")
+    ap.add_argument("--weak", action="store_true",
+                    help="16 x N frames per step as the headline (every GPU renders 16 full-frame equivalents per "
+                         "step: weak scaling in samples, fixed resolution)")
+    ap.add_argument("--strong", action="store_true", help="(the default) 16 frames per step for any N")
     ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--interactive-frames", type=int, default=30,
                     help="frames of the one-frame-per-call measurement (0: skip)")
     ap.add_argument("--strong-steps", type=int, default=20,
-                    help="steps of the fixed 16-frames-per-step measurement reported under 'strong' (0: skip)")
+                    help="steps of the secondary measurement (N > 1: the 16 x N-frame steps under 'samples_weak', "
+                         "and the one-GPU 16-frame reference of 'strong'; 0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roof", action="store_true", help="skip the vector-memory roof micro-benchmark")
     ap.add_argument("--check-launch", action="store_true",
@@ -271,8 +275,8 @@ def main():
     CFG = args.config
     scene = scenes.make_scene(CFG)
     W, H = scene["width"], scene["height"]
-    F = args.frames_per_step or (16 if args.strong else 16 * world)
-    scaling = "strong" if (args.strong or (args.frames_per_step and world > 1)) else "weak"
+    F = args.frames_per_step or (16 * world if args.weak else 16)
+    scaling = "weak" if (args.weak and world > 1) else "strong"
 
     r = VRendererHIP(gpu)
     scenes.load_into(r, scene)
@@ -352,8 +356,8 @@ def main():
         return float(tt.item())
 
     # fixed cadence: 16 frames per step (per gather) whatever N -- the
-    # strong-scaling view of the same job -- against the 1-GPU rate of the
-    # same 16-frame step, measured on every GPU at once over the whole image
+    # headline by default -- against the 1-GPU rate of the same 16-frame
+    # step, measured on every GPU at once over the whole image
     strong = None
     if args.strong_steps > 0:
         SF = 16
@@ -379,6 +383,25 @@ def main():
         strong["note"] = ("16 frames per step and per RCCL gather for any N (fixed display cadence); efficiency = "
                           "value / (N x one_gpu_value), one_gpu_value = the same 16-frame step over the whole "
                           "image on one GPU, measured in this run on every GPU at once")
+
+    # samples-weak view: 16 x N frames per step (every GPU renders 16 full-
+    # frame equivalents per gather), secondary unless --weak made it the headline
+    samples_weak = None
+    if world > 1 and args.strong_steps > 0:
+        WF = 16 * world
+        if F != WF:
+            r.clearBuffer()
+            tw = timed_steps(r, WF, args.strong_steps, scene["time"] + 700000)
+            n_w = args.strong_steps
+        else:
+            tw, n_w = elapsed, args.steps
+        samples_weak = {"frames_per_step": WF, "steps": n_w,
+                        "value": round(wr * hr * 2 * WF * n_w / tw / 1e6, 3),
+                        "ms_per_step": round(tw / n_w * 1e3, 4)}
+        if strong:
+            samples_weak["efficiency"] = round(samples_weak["value"] / (world * strong["one_gpu_value"]), 4)
+        samples_weak["note"] = ("16 x N frames per step and per RCCL gather (every GPU renders 16 full-frame "
+                                "equivalents per step); efficiency against the same one_gpu_value as 'strong'")
 
     # interactive cadence: one frame per synchronous render() call (+ gather)
     inter = None
@@ -548,6 +571,7 @@ def main():
                            "mrays_per_s_traced counts the rays the kernels trace (a pixel's camera ray once "
                            "per launch: no camera jitter, PathTracer.cu:842-844)"),
             "strong": strong,
+            "samples_weak": samples_weak,
             "interactive": inter,
             "roofline": roofline,
         }

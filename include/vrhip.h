@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define VRHIP_ABI_VERSION 2
+#define VRHIP_ABI_VERSION 3
 
 typedef enum vrhip_status {
     VRHIP_OK = 0,
@@ -236,9 +236,32 @@ int vrhip_set_overlap(vrhip_ctx *ctx, int mode);
  * mode 1: every production mesh launch; 0: never; -1 (default, also
  * VRHIP_SERVICE): launches that overlap on the path streams (fewer than 2^24
  * paths, or 2^25 on a tiled rank) when the previous launch is still in flight
- * -- unsynchronised back-to-back calls, not the first call of a burst.  The
- * open session's kernel retires after 20 ms without a new launch. */
+ * -- unsynchronised back-to-back calls, not the first call of a burst; also
+ * whole frames of HDRI mesh scenes behind a launch in flight.  Launches whose
+ * result slots the service's scratch budget (VRHIP_SERVICE_BYTES, default 24
+ * GiB) cannot hold twice take the ordinary launch path in every mode.  The
+ * open session's kernel retires after 20 ms without a new launch; a launch
+ * posted while it retires is detected (a store-fence-load hand-shake on the
+ * ring) and rendered through the launch path instead.  Deferred gathers:
+ * the ncclGather of a vrhip_comm_gather inside a session is enqueued when the
+ * session closes -- at the latest by the next vrhip call on the context that is
+ * not vrhip_render or vrhip_comm_gather, so a rank must call vrhip_sync (or any
+ * read-back) before it blocks in a host-side barrier with the other ranks. */
 int vrhip_set_service(vrhip_ctx *ctx, int mode);
+/* Render-service timing (test hook, no reference counterpart; 0 = default):
+ * the session kernel's idle limit (20 ms), the host's window for posting to
+ * an open session after its last post (5 ms), and a host delay inserted
+ * between that window check and the post -- with a delay longer than the idle
+ * limit every post after a session's first meets a retired kernel, which
+ * exercises the hand-shake above.  Each at most 10 s. */
+int vrhip_set_service_timing(vrhip_ctx *ctx, uint32_t idle_us, uint32_t post_window_us, uint32_t post_delay_us);
+/* Scratch budget of the render service's launch slots on this context
+ * (bytes; 0 = VRHIP_SERVICE_BYTES or 24 GiB).  A launch whose slot the budget
+ * cannot hold twice takes the ordinary launch path. */
+int vrhip_set_service_budget(vrhip_ctx *ctx, size_t bytes);
+/* Launches that met a retiring session kernel and took the launch path
+ * instead (since the context was created). */
+int vrhip_service_stats(vrhip_ctx *ctx, uint64_t *refused_launches);
 /* Frames rendered since the last clear (vRendererCuda::getFrameCount,
  * include/vRendererCuda.h:124). */
 int vrhip_frame_count(vrhip_ctx *ctx, uint32_t *frames);
@@ -293,14 +316,17 @@ int vrhip_comm_init(vrhip_ctx *ctx, uint32_t rank, uint32_t n_ranks, const uint8
  * 2 depth8), ONE ncclGather brings them to rank 0, and rank 0 scatters them
  * into its full image -- all enqueued on the context stream behind the
  * render's finish passes (no host synchronisation).  Rank 0's image `what`
- * then holds the whole frame. */
+ * then holds the whole frame.  Inside a render-service session the gather is
+ * deferred to the session's close (vrhip_set_service): call vrhip_sync before
+ * any host-side barrier between ranks. */
 int vrhip_comm_gather(vrhip_ctx *ctx, int what);
 /* Leaves the communicator (waits for the context stream first).  vrhip_destroy does it too. */
 int vrhip_comm_destroy(vrhip_ctx *ctx);
 
 /* ---- diagnostics ------------------------------------------------------ */
 /* Kernel time of the last vrhip_render (ms, HIP events on the context stream;
- * requires vrhip_sync first). */
+ * requires vrhip_sync first).  After a render-service session: the session's
+ * span, from its kernel's start to its finish pass's end (all its launches). */
 int vrhip_last_kernel_ms(vrhip_ctx *ctx, float *ms);
 /* Accumulated render-kernel time (ms) and launch count since the last reset,
  * from HIP events recorded around every launch's render kernels

@@ -124,6 +124,10 @@ def test_bench_two_ranks_gloo_rehearsal(native):
     st = out["strong"]
     assert st["frames_per_step"] == 16 and st["value"] > 0 and st["one_gpu_value"] > 0
     assert abs(st["efficiency"] - st["value"] / (2 * st["one_gpu_value"])) < 1e-3
+    # the samples-weak view (16 x N frames per step) as a secondary field
+    sw = out["samples_weak"]
+    assert sw["frames_per_step"] == 32 and sw["value"] > 0
+    assert abs(sw["efficiency"] - sw["value"] / (2 * st["one_gpu_value"])) < 1e-3
     # kernel time is the union of overlapping launch spans: never more than the step
     assert out["roofline"]["avg_launch_ms"] <= out["ms_per_step"] * 1.001
 

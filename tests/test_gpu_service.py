@@ -152,3 +152,133 @@ def test_service_kernel_stats_count_every_launch(native):
     ms, n = r.kernel_stats()
     r.cleanUp()
     assert n == 5 and ms > 0.0
+
+
+@pytest.mark.parametrize("cfg,calls,frames", [
+    ("C3", 4, 16),      # 1280x720: 4 back-to-back 16-frame launches, 32 paths per slot, pixel list beyond 1,024 runs
+    ("C5", 2, 16),      # 3840x2160 1M-triangle knot: 2 launches of 66 M paths, 64 queue heads
+])
+def test_service_session_full_size_equals_launch_by_launch(native, oracle, cfg, calls, frames):
+    """The render-service path that produces the C3 / C5 bench numbers, at the
+    BASELINE size and cadence: `calls` back-to-back async 16-frame calls in
+    ONE session (service mode 1) equal the same calls launch by launch
+    (service mode 0) bit for bit -- accum, RGBA8, depth -- so the session's
+    slot layout, its multi-slot finish pass and the listed-pixel runs are
+    exercised at full scale.  C5 also checks the session's image against the
+    glibc oracle over a 48-row band of the 4K frame (the tolerance of
+    test_gpu_parity's baseline-size test, over all the session's frames)."""
+    sc = scenes.make_scene(cfg)
+
+    def run(service):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_service(service)
+        t = sc["time"]
+        kinds = []
+        for i in range(calls):
+            r.render(frames=frames, times=[t + frames * i + k for k in range(frames)], sync=False)
+            kinds.append(r.last_launch_info()["kind"])
+        out = r.read_accum(), r.read_rgba8(), r.read_depth8(), r.getFrameCount()
+        r.cleanUp()
+        return out, kinds
+    (a1, r1, d1, n1), k1 = run(1)
+    (a0, r0, d0, n0), k0 = run(0)
+    assert set(k1) == {"service"} and "service" not in k0, (k1, k0)
+    assert n1 == n0 == calls * frames
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8"); _eq(d1, d0, "depth8")
+    if cfg == "C5":
+        TOL_RMSE, TOL_PIX_FRAC = 1e-3, 0.995      # test_gpu_parity.py's north-star tolerance
+        r0_, r1_ = 1056, 1104
+        nf = calls * frames
+        times = [sc["time"] + k for k in range(nf)]
+        oa, _, _, _ = po.render(sc, frames=nf, times=times, libm=po.LIBM_GLIBC, rows=(r0_, r1_))
+        g = a1[r0_:r1_, :(sc["width"] // 16) * 16, :3] / nf
+        o = oa[r0_:r1_, :(sc["width"] // 16) * 16, :3] / nf
+        assert np.any(o != 0)
+        d = np.abs(g - o).max(-1)
+        rmse = float(np.sqrt(((g - o) ** 2).mean()))
+        frac = float((d <= 1e-3).mean())
+        print(f"C5 session rows {r0_}-{r1_} {nf} frames vs glibc oracle: RMSE {rmse:.3e}, {frac:.6f} within 1e-3")
+        assert rmse < TOL_RMSE, rmse
+        assert frac >= TOL_PIX_FRAC, frac
+
+
+def test_service_retire_race_forced(native):
+    """The lost-launch race, forced: the session kernel retires after 1 ms
+    without a launch, the host's post window is 50 ms and the host sleeps 3 ms
+    between that window check and every post, so posts meet a retiring
+    kernel.  The store-fence-load hand-shake must hand each such launch to the
+    launch path (counted by vrhip_service_stats), the consumed-count check at
+    sync must pass, and the image must equal launch-by-launch rendering."""
+    sc = scenes.make_scene("C3", 96, 64)
+    calls = [2, 1, 3, 2, 1, 2]
+
+    def run(service, timing):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_service(service)
+        if timing:
+            r.set_service_timing(*timing)
+        t = sc["time"]
+        for n in calls:
+            r.render(frames=n, times=[t + k for k in range(n)], sync=False)
+            t += n
+        r.sync()
+        out = r.read_accum(), r.read_rgba8(), r.read_depth8(), r.getFrameCount()
+        refused = r.service_refused()
+        r.cleanUp()
+        return out, refused
+    (a1, r1, d1, n1), refused = run(1, (1000, 50000, 3000))
+    (a0, r0, d0, n0), none = run(0, None)
+    assert refused >= 1 and none == 0, (refused, none)
+    assert n1 == n0 == sum(calls)
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8"); _eq(d1, d0, "depth8")
+
+
+@pytest.mark.parametrize("mode", [-1, 1])
+def test_service_budget_falls_back_to_launch_path(native, mode):
+    """Launches whose result slot the service's scratch budget cannot hold
+    twice take the ordinary launch path in every mode instead of failing
+    (round 4 returned VRHIP_ERR_NOMEM): C3 1280x720 calls of 64 frames (1.4 GB
+    per slot) behind a launch in flight, with a 1 GiB budget.  The image
+    equals launch-by-launch rendering."""
+    sc = scenes.make_scene("C3")
+
+    def run(service, budget):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_service(service)
+        r.set_service_budget(budget)
+        t = sc["time"]
+        kinds = []
+        for i in range(3):
+            r.render(frames=64, times=[t + 64 * i + k for k in range(64)], sync=False)
+            kinds.append(r.last_launch_info()["kind"])
+        out = r.read_accum(), r.read_rgba8()
+        r.cleanUp()
+        return out, kinds
+    (a1, r1), k1 = run(mode, 1 << 30)
+    (a0, r0), _ = run(0, 0)
+    assert "service" not in k1, k1
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8")
+
+
+def test_service_4k_hdri_mesh_64_frame_calls(native):
+    """The advisor's case: back-to-back 64-frame calls of the 4K HDRI-mesh
+    scene in automatic mode (two launch slots of 12.8 GB fit the default
+    24 GiB budget, so they join a session) render without error and equal
+    launch-by-launch rendering."""
+    sc = scenes.make_scene("C5")
+
+    def run(service):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_service(service)
+        t = sc["time"]
+        for i in range(2):
+            r.render(frames=64, times=[t + 64 * i + k for k in range(64)], sync=False)
+        out = r.read_accum(), r.read_rgba8()
+        r.cleanUp()
+        return out
+    (a1, r1), (a0, r0) = run(-1), run(0)
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8")

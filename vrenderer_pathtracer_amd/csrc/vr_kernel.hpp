@@ -1851,6 +1851,16 @@ __device__ __forceinline__ void svc_store_path(const RenderParams& p, uint32_t L
 // svc_idle_ticks without a new launch, the session's retirement -- until
 // the session is closed.  The host writes `closed` only after its last post
 // and this reads `closed` before `posted`, so a close carries the final count.
+// Retiring on its own, the wave first announces it in the host ring's
+// `retired` word, then reads `posted` once more (a store-fence-load pair
+// against svc_post's): a launch posted meanwhile is either seen here and
+// served, or the host sees `retired` and renders it elsewhere (it then
+// excludes the launch's slot from the session's finish pass).  On every exit
+// `retired` holds the launches consumed, which the host checks.
+__device__ __forceinline__ void svc_publish(const RenderParams& p, uint32_t v, int lane)
+{
+    if (lane == 0) __hip_atomic_store(&p.svc_host->retired, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void svc_ring_wave(const RenderParams& p, int lane)
 {
     SvcDevCtl* const d = p.svc_dev;
@@ -1878,10 +1888,26 @@ __device__ __forceinline__ void svc_ring_wave(const RenderParams& p, int lane)
             if (lane == 0) atomicMax(&d->ctl, hp | (hc ? kSvcClosed : 0u));
             dp = hp;
             last = now;
-            if (hc) return;
-        } else if (hc != 0u || now - last > p.svc_idle_ticks) {
-            if (lane == 0) atomicMax(&d->ctl, dp | kSvcClosed);    // closed by the host, or retired when idle
+            if (hc) { svc_publish(p, dp | kSvcClosed, lane); return; }
+        } else if (hc != 0u) {                             // closed by the host
+            if (lane == 0) atomicMax(&d->ctl, dp | kSvcClosed);
+            svc_publish(p, dp | kSvcClosed, lane);
             return;
+        } else if (now - last > p.svc_idle_ticks) {        // idle: retire, unless a launch races it
+            svc_publish(p, dp | kSvcClosed, lane);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+            uint32_t hp2 = 0;
+            if (lane == 0) hp2 = __hip_atomic_load(&p.svc_host->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            hp2 = __builtin_amdgcn_readfirstlane(hp2);
+            if (hp2 <= dp) {
+                if (lane == 0) atomicMax(&d->ctl, dp | kSvcClosed);
+                return;
+            }
+            // serve it (mirrored next round); the host may already have seen
+            // the announcement, then it renders the launch elsewhere as well
+            svc_publish(p, 0u, lane);
+            last = now;
+            continue;
         }
         __builtin_amdgcn_s_sleep(32);
     }
@@ -1892,9 +1918,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
 {
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
-#if VR_X != 1
     if (blockIdx.x == 0u && (tid >> 6) == BT / 64 - 1) { svc_ring_wave(p, lane); return; }
-#endif
     constexpr bool SPARSE = (FEAT & F_SPARSE) != 0u;       // the session's listed pixels only
     // chunk rows: 8x8 sub-tiles, or (F_SPARSE) runs of 64 pixels the
     // session's primary pass listed (the last run padded, render_wave_kernel)

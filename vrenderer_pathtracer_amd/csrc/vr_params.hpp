@@ -97,10 +97,17 @@ struct SvcLaunch {                                 // one launch of a session (2
     uint32_t times[kMaxFramesPerLaunch];
 };
 constexpr uint32_t kSvcLaunchWords = (uint32_t)(sizeof(SvcLaunch) / 4);
-struct SvcHostCtl {                                // host-pinned (coherent), written by the host only
-    uint32_t posted;                               // launches posted: desc[0, posted) are valid
-    uint32_t closed;                               // 1: no launch follows `posted` (written after it)
-    uint32_t pad[30];
+struct SvcHostCtl {                                // host-pinned (coherent)
+    uint32_t posted;                               // host: launches posted, desc[0, posted) are valid
+    uint32_t closed;                               // host: 1 = no launch follows `posted` (written after it)
+    uint32_t pad0[30];
+    // device (the ring wave): 0 while the kernel serves; launches consumed |
+    // kSvcClosed once it stops.  Retiring on its own (idle) it writes this
+    // BEFORE its last look at `posted`, and the host reads it AFTER storing
+    // `posted` (svc_post), so a launch posted as the kernel retires is seen
+    // as taken by exactly one side (svc_ring_wave, vrhip_api.cpp svc_post)
+    uint32_t retired;
+    uint32_t pad1[31];
     SvcLaunch desc[kSvcMaxLaunches];
 };
 constexpr uint32_t kSvcClosed = 0x80000000u;

@@ -21,6 +21,7 @@
 #include <array>
 #include <queue>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -159,6 +160,11 @@ struct vrhip_ctx {
         hipEvent_t ring_done[2] = { nullptr, nullptr };
         bool ring_used[2] = { false, false };
         uint32_t ring_i = 0;
+        uint32_t cur_ring = 0;                    // the open (or last) session's ring
+        // per ring: the launches its last session summed, and whether the
+        // kernel's count of consumed launches (SvcHostCtl::retired) was checked
+        uint32_t ring_posted[2] = { 0, 0 };
+        bool ring_checked[2] = { true, true };
         vr::SvcHostCtl* host = nullptr;           // the open session's ring
         vr::SvcDevCtl* dev = nullptr;             // device mirror of the ring
         uint32_t* qctl = nullptr; size_t qctl_slots = 0;    // work-queue heads per launch slot
@@ -180,6 +186,12 @@ struct vrhip_ctx {
         bool finished_used = false;
     } svc;
     int service = -1;                             // 1 every production mesh launch, 0 never, -1 automatic
+    // vrhip_set_service_timing (test hook; 0 = default): the kernel's idle
+    // limit, the host's post window, a host delay between the window check
+    // and the post (forces the retire-vs-post race)
+    uint32_t svc_idle_us = 0, svc_window_us = 0, svc_post_delay_us = 0;
+    uint64_t svc_refused = 0;                     // launches a retiring session kernel did not take
+    size_t svc_budget = 0;                        // vrhip_set_service_budget (0: VRHIP_SERVICE_BYTES / 24 GiB)
     // multi-device renderer (vrhip_create_multi): the lead context holds every
     // member context (itself first); settings fan out to all of them
     std::vector<vrhip_ctx*> group;
@@ -1047,6 +1059,47 @@ static vr::RenderParams svc_key(const vr::RenderParams& p)
     return k;
 }
 
+// Launch slots a session of launches of up to kmax frames gets (0 or 1:
+// the service cannot take such launches; they take the launch path).  The
+// scratch budget (VRHIP_SERVICE_BYTES, default 24 GiB of the 288 GiB HBM)
+// holds every slot's path results: 24 B per pixel and frame.
+static uint32_t svc_slots(const vrhip_ctx* c, uint32_t path_stride, uint32_t kmax, size_t* slot_bytes_out)
+{
+    const size_t stride = path_stride;
+    const size_t slot_bytes = ((12u * 2u * (size_t)kmax * stride + 4u * stride) + 255u) & ~(size_t)255u;
+    static const size_t env_budget = [] {
+        const char* e = std::getenv("VRHIP_SERVICE_BYTES");
+        return e ? (size_t)std::atoll(e) : ((size_t)24 << 30);
+    }();
+    const size_t budget = c->svc_budget ? c->svc_budget : env_budget;
+    if (slot_bytes_out) *slot_bytes_out = slot_bytes;
+    return (uint32_t)std::min<size_t>(vr::kSvcMaxLaunches, budget / slot_bytes);
+}
+
+// The kernel of ring ri's last session has finished: it must have consumed
+// every launch the session's finish pass summed (svc_post's hand-shake makes
+// that so; this check makes any breach loud instead of a silently wrong image).
+static int svc_check_ring(vrhip_ctx* c, uint32_t ri)
+{
+    auto& S = c->svc;
+    if (!S.ring_used[ri] || S.ring_checked[ri] || (S.open && S.cur_ring == ri)) return VRHIP_OK;
+    HIP_TRY(hipEventSynchronize(S.ring_done[ri]));
+    S.ring_checked[ri] = true;
+    const uint32_t r = __atomic_load_n(&S.rings[ri]->retired, __ATOMIC_ACQUIRE);
+    if ((r & vr::kSvcClosed) == 0u || (r & ~vr::kSvcClosed) < S.ring_posted[ri])
+        return fail(VRHIP_ERR_HIP, "render service: the kernel consumed " + std::to_string(r & ~vr::kSvcClosed) +
+                                       " of " + std::to_string(S.ring_posted[ri]) + " launches");
+    return VRHIP_OK;
+}
+// after a host synchronisation: both rings' finished sessions
+static int svc_verify(vrhip_ctx* c)
+{
+    int rc;
+    for (uint32_t ri = 0; ri < 2; ++ri)
+        if ((rc = svc_check_ring(c, ri)) != VRHIP_OK) return rc;
+    return VRHIP_OK;
+}
+
 // Closes the open session: the kernel retires once the ring is drained, then
 // the finish pass and the deferred gathers run on `stream`.  Asynchronous.
 static int svc_close(vrhip_ctx* c)
@@ -1055,7 +1108,11 @@ static int svc_close(vrhip_ctx* c)
     if (!S.open) return VRHIP_OK;
     S.open = false;
     __atomic_store_n(&S.host->closed, 1u, __ATOMIC_RELEASE);
+    S.ring_posted[S.cur_ring] = S.posted;
+    S.ring_checked[S.cur_ring] = false;
     HIP_TRY(hipStreamWaitEvent(c->stream, S.k1, 0));
+    // the launches the host posted and the kernel took (svc_post): a launch
+    // that met a retiring kernel was not counted and went the launch path
     S.fin.n = S.posted;
     const int e = vr::launch_service_finish(S.p, S.fin, S.n_tiles, c->stream);
     if (e != 0) return fail(VRHIP_ERR_HIP, std::string("service finish launch: ") + hipGetErrorString((hipError_t)e));
@@ -1082,6 +1139,9 @@ static int svc_close(vrhip_ctx* c)
     S.gathers.clear();
     HIP_TRY(hipEventRecord(S.finished, c->stream));
     S.finished_used = true;
+    // vrhip_last_kernel_ms after a session: its span, kernel start to finish pass
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
     // the session's kernel span: one span covering all its launches
     hipEvent_t a = nullptr, b = nullptr;
     if ((a = S.k0) && (b = S.k1)) {
@@ -1109,14 +1169,14 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     // kernel (two sessions back) must have retired before the host rewrites it
     const uint32_t ri = S.ring_i;
     S.ring_i ^= 1u;
-    if (S.ring_used[ri]) HIP_TRY(hipEventSynchronize(S.ring_done[ri]));
+    int rc;
+    if (S.ring_used[ri]) {
+        HIP_TRY(hipEventSynchronize(S.ring_done[ri]));
+        if ((rc = svc_check_ring(c, ri)) != VRHIP_OK) return rc;
+    }
     const size_t stride = p.path_stride;
-    const size_t slot_bytes = ((12u * 2u * (size_t)kmax * stride + 4u * stride) + 255u) & ~(size_t)255u;
-    static const size_t budget = [] {
-        const char* e = std::getenv("VRHIP_SERVICE_BYTES");
-        return e ? (size_t)std::atoll(e) : ((size_t)8 << 30);
-    }();
-    const uint32_t slots = (uint32_t)std::min<size_t>(vr::kSvcMaxLaunches, budget / slot_bytes);
+    size_t slot_bytes = 0;
+    const uint32_t slots = svc_slots(c, p.path_stride, kmax, &slot_bytes);
     if (slots < 2) return fail(VRHIP_ERR_NOMEM, "render service: the budget holds fewer than 2 launch slots");
     const uint32_t stage_px = owned_tiles_of(c->W, c->H, 0, c->nranks) * 256u;   // rank 0 owns the most tiles
     const size_t stage_bytes = (24u * (size_t)stage_px + 255u) & ~(size_t)255u;
@@ -1131,7 +1191,6 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
         cap = need;
         return VRHIP_OK;
     };
-    int rc;
     if ((rc = grow(S.scratch, S.scratch_cap, (size_t)slots * slot_bytes)) != VRHIP_OK) return rc;
     if ((rc = grow(S.prim, S.prim_cap, 32u * stride)) != VRHIP_OK) return rc;
     if ((rc = grow(S.staging, S.staging_cap, (size_t)slots * stage_bytes)) != VRHIP_OK) return rc;
@@ -1148,45 +1207,59 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     S.p.prim = S.prim;
     S.p.sparse_px = sparse ? S.subs : nullptr;
     S.host = S.rings[ri];
+    S.cur_ring = ri;
     S.p.svc_host = S.rings_dev[ri]; S.p.svc_dev = S.dev; S.p.svc_qctl = S.qctl;
     S.p.svc_slot_bytes = slot_bytes; S.p.svc_kmax = kmax;
-    S.p.svc_idle_ticks = (uint32_t)VR_SVC_IDLE_MS * 100000u;
+    S.p.svc_idle_ticks = (c->svc_idle_us ? c->svc_idle_us : (uint32_t)VR_SVC_IDLE_MS * 1000u) * 100u;   // 100 MHz
     S.key = svc_key(p);
     std::memset(&S.fin, 0, sizeof(S.fin));
     S.fin.first_frame = c->frame;
     S.fin.staging = S.staging; S.fin.stage_bytes = stage_bytes; S.fin.stage_pixels = stage_px;
     S.gathers.clear();
-    // the ring: nothing posted, open (the kernel launch below orders these
-    // host stores before the kernel's first read)
-    S.host->posted = 0; S.host->closed = 0;
+    // the ring: nothing posted, open, the kernel serving (the kernel launch
+    // below orders these host stores before the kernel's first read)
+    S.host->posted = 0; S.host->closed = 0; S.host->retired = 0;
     // everything queued on `stream` first (uploads, clears, earlier finish passes)
     HIP_TRY(hipEventRecord(c->ev_join, c->stream));
     HIP_TRY(hipStreamWaitEvent(S.s, c->ev_join, 0));
     HIP_TRY(hipMemsetAsync(S.dev, 0, sizeof(vr::SvcDevCtl), S.s));
     HIP_TRY(hipMemsetAsync(S.qctl, 0, (size_t)slots * vr::kSvcQctlWords * 4u, S.s));
     HIP_TRY(hipEventRecord(S.k0, S.s));
+    HIP_TRY(hipEventRecord(c->ev0, S.s));
     const int e = vr::launch_service(S.p, n_tiles, stack, S.s);
     if (e != 0) return fail(VRHIP_ERR_HIP, std::string("service launch: ") + hipGetErrorString((hipError_t)e));
     HIP_TRY(hipEventRecord(S.k1, S.s));
     HIP_TRY(hipEventRecord(S.ring_done[ri], S.s));
     S.ring_used[ri] = true;
+    S.ring_checked[ri] = false;
+    S.ring_posted[ri] = 0;
     S.open = true;
     S.last_post = std::chrono::steady_clock::now();
     return VRHIP_OK;
 }
 
 // Posts one launch of k frames (first frame c->frame) to the open session.
-static void svc_post(vrhip_ctx* c, uint32_t k, const uint32_t* times, uint32_t time_seed)
+// false: the session's kernel was retiring (idle) and did not take it -- the
+// caller closes the session without it and renders it another way.  The
+// hand-shake with svc_ring_wave: the host stores `posted`, fences, reads
+// `retired`; the kernel stores `retired`, fences, reads `posted`.  Whichever
+// store is first, the other side's load sees it, so the launch is taken by
+// the kernel (it saw `posted`) or by the caller (it saw `retired`) -- never
+// by neither.
+static bool svc_post(vrhip_ctx* c, uint32_t k, const uint32_t* times, uint32_t time_seed)
 {
     auto& S = c->svc;
     vr::SvcLaunch& d = S.host->desc[S.posted];
     d.first_frame = c->frame;
     d.n_frames = k;
     for (uint32_t i = 0; i < k; ++i) d.times[i] = times ? times[i] : time_seed;
+    __atomic_store_n(&S.host->posted, S.posted + 1u, __ATOMIC_SEQ_CST);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    if (__atomic_load_n(&S.host->retired, __ATOMIC_SEQ_CST) != 0u) return false;
     S.fin.n_frames[S.posted] = k;
-    __atomic_store_n(&S.host->posted, S.posted + 1u, __ATOMIC_RELEASE);
     ++S.posted;
     S.last_post = std::chrono::steady_clock::now();
+    return true;
 }
 
 // Whether the open session can take a launch of k frames with parameters p.
@@ -1195,7 +1268,8 @@ static bool svc_fits(const vrhip_ctx* c, const vr::RenderParams& p, uint32_t k)
     const auto& S = c->svc;
     if (!S.open || S.posted >= S.slots || k > S.kmax) return false;
     const auto idle = std::chrono::steady_clock::now() - S.last_post;
-    if (idle > std::chrono::milliseconds(VR_SVC_POST_MS)) return false;
+    const uint32_t window_us = c->svc_window_us ? c->svc_window_us : (uint32_t)VR_SVC_POST_MS * 1000u;
+    if (idle > std::chrono::microseconds(window_us)) return false;
     const vr::RenderParams key = svc_key(p);
     return std::memcmp(&key, &S.key, sizeof(key)) == 0;
 }
@@ -1267,6 +1341,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     const bool wave_kernel = (f & vr::F_MESH) != 0u;   // mesh scenes: the path-pool kernel (scratch + finish pass)
     (void)hipGetLastError();            // launches below report their own errors only
     // counting launches and anything else than a production mesh launch end a session first
+    uint32_t done = 0;                  // frames rendered by the service below (the launch path takes the rest)
     {
         const size_t paths_k = (size_t)p.path_stride * 2u * k_max;
         const bool ovl_size = paths_k < ((size_t)1 << 24) || (c->nranks > 1 && paths_k < ((size_t)1 << 25));
@@ -1276,8 +1351,11 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // C3 16,505 -> 18,948, C5 21,630 -> 22,171 Mpaths/s; the Cornell box's
         // whole frames lose, C2 4,111 -> 4,021, and keep the shard-size limit)
         const bool svc_size = ovl_size || (VR_SERVICE_HDRI_FRAMES != 0 && !c->cornell);
+        // launches whose slots the scratch budget cannot hold twice take the
+        // launch path in every mode (4K frames of many frames per launch)
         const bool svc = count == 0 && wave_kernel && stack <= 32 && n_tiles > 0 &&
-                         (c->service > 0 || (c->service < 0 && svc_size && in_flight && c->overlap != 0));
+                         (c->service > 0 || (c->service < 0 && svc_size && in_flight && c->overlap != 0)) &&
+                         svc_slots(c, p.path_stride, k_max, nullptr) >= 2u;
         if (!svc) {
             if ((rc = svc_close(c)) != VRHIP_OK) return rc;
         } else {
@@ -1288,21 +1366,31 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
                 return (q >= 8 && q <= (uint32_t)VR_MAX_QUEUES && (q & (q - 1)) == 0) ? q : 0u;
             }();
             if (env_q) p.n_queues = env_q;
-            uint32_t done = 0;
+            bool refused = false;
             while (done < n_frames) {
                 const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
                 if (c->svc.open && !svc_fits(c, p, k) && (rc = svc_close(c)) != VRHIP_OK) return rc;
                 if (!c->svc.open && (rc = svc_open(c, p, stack, n_tiles, k_max)) != VRHIP_OK) return rc;
-                svc_post(c, k, times ? times + done : nullptr, time_seed);
+                if (c->svc_post_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(c->svc_post_delay_us));
+                if (!svc_post(c, k, times ? times + done : nullptr, time_seed)) {
+                    // the session's kernel retired as this launch was posted:
+                    // close the session without it; this call's remaining
+                    // frames take the launch path below
+                    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
+                    refused = true;
+                    ++c->svc_refused;
+                    break;
+                }
                 c->frame += k;
                 done += k;
             }
-            c->last_split = 1; c->last_use_scratch = 1; c->last_kind = 2;
-            return VRHIP_OK;
+            if (!refused) {
+                c->last_split = 1; c->last_use_scratch = 1; c->last_kind = 2;
+                return VRHIP_OK;
+            }
         }
     }
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    uint32_t done = 0;
     while (done < n_frames) {
         const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
         p.first_frame = c->frame;
@@ -1568,7 +1656,7 @@ static int one_sync(vrhip_ctx* c)
     int rc = set_device(c); if (rc) return rc;
     if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return VRHIP_OK;
+    return svc_verify(c);
 }
 
 int vrhip_frame_count(vrhip_ctx* c, uint32_t* frames)
@@ -1585,7 +1673,7 @@ static int readback(vrhip_ctx* c, const void* src, void* dst, size_t bytes)
     if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return VRHIP_OK;
+    return svc_verify(c);
 }
 
 int vrhip_read_accum(vrhip_ctx* c, float* out)
@@ -1636,6 +1724,34 @@ static int one_set_service(vrhip_ctx* c, int mode)
     int rc = set_device(c); if (rc) return rc;
     if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     c->service = mode;
+    return VRHIP_OK;
+}
+
+int vrhip_set_service_timing(vrhip_ctx* c, uint32_t idle_us, uint32_t post_window_us, uint32_t post_delay_us)
+{
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_set_service_timing");
+    if (!c || idle_us > 10000000u || post_window_us > 10000000u || post_delay_us > 10000000u)
+        return fail(VRHIP_ERR_INVALID, "bad service timing (each at most 10 s)");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
+    c->svc_idle_us = idle_us; c->svc_window_us = post_window_us; c->svc_post_delay_us = post_delay_us;
+    return VRHIP_OK;
+}
+
+int vrhip_set_service_budget(vrhip_ctx* c, size_t bytes)
+{
+    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_set_service_budget");
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    int rc = set_device(c); if (rc) return rc;
+    if ((rc = svc_close(c)) != VRHIP_OK) return rc;
+    c->svc_budget = bytes;
+    return VRHIP_OK;
+}
+
+int vrhip_service_stats(vrhip_ctx* c, uint64_t* refused_launches)
+{
+    if (!c || !refused_launches) return fail(VRHIP_ERR_INVALID, "null argument");
+    *refused_launches = c->svc_refused;
     return VRHIP_OK;
 }
 

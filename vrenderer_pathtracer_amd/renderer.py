@@ -359,6 +359,23 @@ class VRendererHIP:
         kernel): 1 always, 0 never, -1 automatic (vrhip_set_service)."""
         check(self._lib.vrhip_set_service(self._need_ctx(), int(mode)), "vrhip_set_service")
 
+    def set_service_timing(self, idle_us: int = 0, post_window_us: int = 0, post_delay_us: int = 0) -> None:
+        """Test hook (vrhip_set_service_timing): the session kernel's idle
+        limit, the host's post window and a host delay before each post
+        (0 = default)."""
+        check(self._lib.vrhip_set_service_timing(self._need_ctx(), int(idle_us), int(post_window_us),
+                                                 int(post_delay_us)), "vrhip_set_service_timing")
+
+    def set_service_budget(self, nbytes: int = 0) -> None:
+        """Scratch budget of the render service's launch slots (0: default)."""
+        check(self._lib.vrhip_set_service_budget(self._need_ctx(), int(nbytes)), "vrhip_set_service_budget")
+
+    def service_refused(self) -> int:
+        """Launches that met a retiring session kernel and took the launch path."""
+        n = ctypes.c_uint64(0)
+        check(self._lib.vrhip_service_stats(self._need_ctx(), ctypes.byref(n)), "vrhip_service_stats")
+        return int(n.value)
+
     def owned_pixels(self) -> int:
         """Pixels this rank renders (256 per owned 16x16 tile)."""
         n = ctypes.c_uint32(0)
