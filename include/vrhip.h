@@ -54,13 +54,16 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx **out);
  * repeats), each rendering the 16x16 tiles i, i + n, ... of the image; the
  * RCCL communicators are made in one call (ncclCommInitAll).  The returned
  * context is the lead (devices[0]): every setting and upload on it fans out
- * to all members; vrhip_render renders every device's tiles and gathers the
- * RGBA8 and depth tiles to the lead (one grouped ncclGather each), so the
- * lead's images, read-back and GL presentation show the whole frame;
- * vrhip_read_accum gathers the accumulation first; vrhip_comm_gather gathers
- * the given image.  Refused on it: vrhip_set_tiling, vrhip_set_stream,
- * vrhip_comm_init/destroy, vrhip_set_service, the counting renders.  n = 1 is
- * allowed (the same code, a one-rank communicator). */
+ * to all members; vrhip_render renders every device's tiles (each member
+ * with its own render service for back-to-back calls, vrhip_set_service), and
+ * the RGBA8 and depth tiles are gathered to the lead (one grouped ncclGather
+ * each) when the lead's images are next needed -- vrhip_read_rgba8/depth8,
+ * vrhip_gl_present, vrhip_device_buffers, vrhip_sync -- so read-back and GL
+ * presentation show the whole frame; vrhip_read_accum gathers the
+ * accumulation first; vrhip_comm_gather gathers the given image.  Refused on
+ * it: vrhip_set_tiling, vrhip_set_stream, vrhip_comm_init/destroy, the
+ * service test hooks, the counting renders.  n = 1 is allowed (the same code,
+ * a one-rank communicator). */
 int vrhip_create_multi(const int *devices, uint32_t n_devices, uint32_t width, uint32_t height, vrhip_ctx **out);
 /* The devices of a context (one for vrhip_create, the group for
  * vrhip_create_multi, lead first); `devices` may be NULL (count only). */

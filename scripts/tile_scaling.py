@@ -11,6 +11,11 @@ For N in 1, 2, 4, 8 this renders rank 0's share of an N-way band split (rank
 whole-job Mpaths/s (full-image paths / rank-0 time, gather excluded) and the
 projected efficiency vs N x the 1-GPU rate.  It isolates the per-rank
 occupancy loss of strong scaling from the gather cost.
+
+TS_SYNC=1: every render call is synchronised (the reference's cadence --
+the Qt host syncs each paint, src/vRendererCuda.cpp:107-165 -- i.e. the
+vRendererHIP adapter on a vrhip_create_multi context with 1 or 4 frames per
+call): the projection of the one-process multi-GPU path, gather excluded.
 """
 import os
 import sys
@@ -49,20 +54,21 @@ for n in NS:
     # of this shape (kernel code loaded, scratch allocated, first-use stream
     # joins done) before the timed steps
     W0 = 6
+    SYNC = os.environ.get("TS_SYNC", "") == "1"
     for i in range(W0):
-        r.render(frames=F, times=[sc["time"] + i * F + k for k in range(F)], sync=False)
+        r.render(frames=F, times=[sc["time"] + i * F + k for k in range(F)], sync=SYNC)
     r.sync()
     r.kernel_stats(reset=True)
     torch.cuda.synchronize()
     steps = STEPS
     t0 = time.perf_counter()
     for i in range(steps):
-        r.render(frames=F, times=[sc["time"] + (W0 + i) * F + k for k in range(F)], sync=False)
+        r.render(frames=F, times=[sc["time"] + (W0 + i) * F + k for k in range(F)], sync=SYNC)
     r.sync()
     dt = (time.perf_counter() - t0) / steps
     kms, launches = r.kernel_stats()
     rate = paths / dt / 1e6
     base = base or rate
-    print(f"{cfg} F={F} split={SPLIT} N={n}: rank-0 px {r.owned_pixels():7d}  step {dt * 1e3:8.3f} ms  kernel {kms / launches:8.3f} ms  "
+    print(f"{cfg} F={F}{' sync' if SYNC else ''} split={SPLIT} N={n}: rank-0 px {r.owned_pixels():7d}  step {dt * 1e3:8.3f} ms  kernel {kms / launches:8.3f} ms  "
           f"projected {rate:9.1f} Mpaths/s  eff {rate / (n * base):.3f}", flush=True)
 r.cleanUp()

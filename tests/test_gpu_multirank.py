@@ -142,17 +142,23 @@ def _single(sc, frames, times):
     return out
 
 
-def _multi(sc, devices, calls, t0):
+def _multi(sc, devices, calls, t0, service=None, sync=True):
     from vrenderer_pathtracer_amd import VRendererHIP, scenes
     r = VRendererHIP(list(devices))
     scenes.load_into(r, sc)
+    if service is not None:
+        r.set_service(service)
     assert r.device_group() == list(devices)
     t = t0
+    kinds = []
     for n in calls:
-        r.render(frames=n, times=[t + k for k in range(n)])
+        r.render(frames=n, times=[t + k for k in range(n)], sync=sync)
+        kinds.append(r.last_launch_info()["kind"])
         t += n
     out = r.read_accum(), r.read_rgba8(), r.read_depth8(), r.getFrameCount()
     r.cleanUp()
+    if service is not None:
+        return out, kinds
     return out
 
 
@@ -178,17 +184,38 @@ def test_multi_context_one_device_bitexact(native, oracle, cfg):
 
 
 def test_multi_context_refuses_per_rank_calls(native):
-    """Tiling, streams, communicators and the render service belong to the
-    multi-device context itself: setting them on it is refused."""
+    """Tiling, streams, communicators and the service test hooks belong to
+    the multi-device context itself: setting them on it is refused (the
+    service mode fans out to the members)."""
     from vrenderer_pathtracer_amd import VRendererHIP, scenes
     from vrenderer_pathtracer_amd._native import VRHIPError
     sc = scenes.make_scene("C2", 64, 64)
     r = VRendererHIP([0])
     scenes.load_into(r, sc)
-    for call in (lambda: r.set_tiling(0, 2), lambda: r.set_service(1)):
+    for call in (lambda: r.set_tiling(0, 2), lambda: r.set_service_timing(1000, 0, 0),
+                 lambda: r.set_service_budget(1 << 30)):
         with pytest.raises(VRHIPError):
             call()
+    r.set_service(1)
     r.cleanUp()
+
+
+@pytest.mark.parametrize("cfg,service", [("C2", 1), ("C3", -1)])
+def test_multi_context_service_burst_bitexact(native, cfg, service):
+    """A burst of unsynchronised render calls on a one-device multi context:
+    the member renders on its render service (one session across the calls:
+    the colour / depth gather waits for the read-back), and the lead's images
+    equal the plain context's bit for bit."""
+    from vrenderer_pathtracer_amd import scenes
+    sc = scenes.make_scene(cfg, 160, 96) if cfg == "C2" else scenes.make_scene(cfg)
+    t = sc["time"]
+    calls = [2, 1, 3, 2, 4]
+    (ga, gr, gd, nf), kinds = _multi(sc, [0], calls, t, service=service, sync=False)
+    assert nf == sum(calls)
+    assert "service" in kinds, kinds
+    sa, sr, sd = _single(sc, sum(calls), [t + k for k in range(sum(calls))])
+    assert np.array_equal(ga.view(np.uint32), sa.view(np.uint32))
+    assert np.array_equal(gr, sr) and np.array_equal(gd, sd)
 
 
 def test_multi_context_two_devices_bitexact(native):

@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(kBlockThreads) svc_finish_kernel(const RenderP
             for (uint32_t q = 0; q < n_paths; ++q) io = add4(io, shared_h);
             last_w = 1.f;
         } else {
-            const float depth = reinterpret_cast<const float*>(base + (size_t)2u * p.svc_kmax * p.path_stride)[slot];
+            const float depth = reinterpret_cast<const float*>(p.paths + (size_t)2u * p.svc_kmax * p.path_stride)[slot];
             const vr3* src = base + slot;
             for (uint32_t q = 0; q < n_paths; ++q) {
                 const vr3 r = src[(size_t)q * p.path_stride];

@@ -809,6 +809,17 @@ __device__ __forceinline__ void path_begin(PathState& ps, uint32_t& s0, uint32_t
     ps.rng.seed(hash_seeds(s0, s1));
 }
 
+// The depth term of a path (PathTracer.cu:656-661): |hit - origin| / 150 of
+// its bounce-0 hit, i.e. of the camera ray's closest hit (no jitter: the same
+// for every path of the pixel).  Path-pool launches with a primary pass take
+// it from primary_kernel, which stores it once per pixel, and their path
+// kernels carry no depth register (bounce_step<..., false>).
+__device__ __forceinline__ float depth_term(const vr4& o, const vr4& hp)
+{
+    const vr4 l = sub4(o, hp);
+    return sqrt_exact(dot4(l, l)) / 150.f;
+}
+
 // Coherence probe (-DVR_PROBE_COHERENT=G; INVALID images, measurement only):
 // the lanes sampling a diffuse / BRDF bounce in the same step are split into
 // G groups of 64/G lanes, and every lane takes its group leader's (first
@@ -835,7 +846,7 @@ __device__ __forceinline__ void probe_coherent(float& rand1, float& rand2)
 // One bounce of trace's loop body (:627-769) for the closest hit `hr` of
 // `ray` (hr.t == 1e20: miss).  Returns true when the path ends, with its
 // radiance (w = depth) in `out`; otherwise `ray` is the next bounce's ray.
-template <bool COUNT, uint32_t FEAT>
+template <bool COUNT, uint32_t FEAT, bool DEPTH = true>
 __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, const HitRec& hr, PathState& ps,
                                             vr4& out, Cnt& cnt)
 {
@@ -902,10 +913,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
             cnt.ld128 += nt;
         }
     }
-    if (ps.bounce == 0) {
-        const vr4 l = sub4(ray.o, h.hp);
-        ps.depth = sqrt_exact(dot4(l, l)) / 150.f;
-    }
+    if (DEPTH && ps.bounce == 0) ps.depth = depth_term(ray.o, h.hp);
     ps.accum = add4(ps.accum, mul4(ps.mask, h.em));
     ray.o = h.hp;
     const vr4 normal = h.n;
@@ -1039,6 +1047,11 @@ __device__ __forceinline__ void store_path(const RenderParams& p, uint32_t q, ui
 {
     p.paths[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
     if (q == 0u) p.path_w[slot] = depth;
+}
+// the radiance only: primary_kernel stored the pixel's depth term
+__device__ __forceinline__ void store_path_rgb(const RenderParams& p, uint32_t q, uint32_t slot, const vr4& out)
+{
+    p.paths[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
 }
 
 // Binds this thread's stack column and fills the block's node cache with
@@ -1267,6 +1280,13 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
     const uint32_t slot = tile * kBlockThreads + (uint32_t)tid;
     vr4* dst = p.prim + 2u * (size_t)slot;
     dst[0] = mk4(hr.t, __int_as_float(hr.kind), __int_as_float(hr.idx), hr.bu);
+    // the pixel's depth term for the path kernel's finish pass (bounce 0 is
+    // this hit for every path; 1 when the camera ray escapes, path_begin)
+    {
+        const float dt = hit ? depth_term(cam.o, add4(cam.o, mul4s(cam.d, hr.t))) : 1.f;
+        if (p.svc_dev) reinterpret_cast<float*>(p.paths + (size_t)2u * p.svc_kmax * p.path_stride)[slot] = dt;
+        else p.path_w[slot] = dt;
+    }
     if constexpr (prim_has_dir<FEAT>())
         dst[1] = mk4(hr.bv, cam.d.x, cam.d.y, cam.d.z);   // the paths reuse the camera ray too
     else
@@ -1787,8 +1807,10 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         bool ended = false;
         if (state == LS_SHADE) {
             vr4 out;
-            if (bounce_step<CNT, FEAT>(p, ray, hr, ps, out, cnt)) {
-                store_path(p, q, slot, out, ps.depth);
+            constexpr bool INL = (FEAT & F_INLINE_PRIM) != 0u;   // the path traced its own camera ray
+            if (bounce_step<CNT, FEAT, INL>(p, ray, hr, ps, out, cnt)) {
+                if constexpr (INL) store_path(p, q, slot, out, ps.depth);
+                else store_path_rgb(p, q, slot, out);
                 if constexpr ((FEAT & F_SMALL) != 0u) {
                     if (p.path_cost)
                         p.path_cost[(size_t)q * p.path_stride + slot] = (uint8_t)(cnt.work < 510u ? cnt.work >> 1 : 255u);
@@ -1837,12 +1859,11 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
 __device__ __forceinline__ uint32_t svc_ld(const uint32_t* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // a path's radiance into its launch's slot (the store_path layout per slot)
-__device__ __forceinline__ void svc_store_path(const RenderParams& p, uint32_t L, uint32_t q, uint32_t slot,
-                                               const vr4& out, float depth)
+// (the pixel's depth term: primary_kernel, once per session, in slot 0)
+__device__ __forceinline__ void svc_store_path(const RenderParams& p, uint32_t L, uint32_t q, uint32_t slot, const vr4& out)
 {
     vr3* const base = reinterpret_cast<vr3*>(reinterpret_cast<uint8_t*>(p.paths) + (size_t)L * p.svc_slot_bytes);
     base[(size_t)q * p.path_stride + slot] = vr3{ out.x, out.y, out.z };
-    if (q == 0u) reinterpret_cast<float*>(base + (size_t)2u * p.svc_kmax * p.path_stride)[slot] = depth;
 }
 
 // The ring wave (the last wave of block 0; it takes no paths): mirrors the
@@ -2091,8 +2112,8 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
         bool ended = false;
         if (state == LS_SHADE) {
             vr4 out;
-            if (bounce_step<false, FEAT>(p, ray, hr, ps, out, cnt)) {
-                svc_store_path(p, q >> 8, q & 0xffu, slot, out, ps.depth);
+            if (bounce_step<false, FEAT, false>(p, ray, hr, ps, out, cnt)) {
+                svc_store_path(p, q >> 8, q & 0xffu, slot, out);
                 ended = true;
             } else {
                 state = LS_SETUP;

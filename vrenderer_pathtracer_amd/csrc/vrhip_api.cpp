@@ -195,6 +195,9 @@ struct vrhip_ctx {
     // multi-device renderer (vrhip_create_multi): the lead context holds every
     // member context (itself first); settings fan out to all of them
     std::vector<vrhip_ctx*> group;
+    // the lead of a group: renders since the colour / depth tiles were last
+    // gathered (the gather runs when the lead's images are next needed)
+    bool group_stale = false;
     // multi-GPU tile gather (vrhip_comm_*): one RCCL communicator per context
     ncclComm_t comm = nullptr;
     uint8_t* comm_send = nullptr;    // this rank's packed tiles (largest element, 16 B/pixel)
@@ -207,6 +210,7 @@ static void svc_free(vrhip_ctx* c);
 static int svc_close(vrhip_ctx* c);
 static int refuse_multi(vrhip_ctx* c, const char* what);
 static int multi_gather(vrhip_ctx* c, int what);
+static int multi_images(vrhip_ctx* c);
 
 namespace {
 
@@ -819,7 +823,8 @@ int vrhip_gl_register_image(vrhip_ctx* c, int which, unsigned int gl_texture, un
 int vrhip_gl_present(vrhip_ctx* c)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
-    int rc = set_device(c); if (rc) return rc;
+    int rc = multi_images(c); if (rc) return rc;
+    if ((rc = set_device(c)) != VRHIP_OK) return rc;
     if ((rc = svc_close(c)) != VRHIP_OK) return rc;
     const void* src[2] = { c->rgba, c->depth };
     for (int i = 0; i < 2; ++i) {
@@ -1685,12 +1690,23 @@ int vrhip_read_accum(vrhip_ctx* c, float* out)
     }
     return readback(c, c->accum, out, (size_t)c->W * c->H * 16);
 }
-int vrhip_read_rgba8(vrhip_ctx* c, uint8_t* out) { return c ? readback(c, c->rgba, out, (size_t)c->W * c->H * 4) : fail(VRHIP_ERR_INVALID, "null ctx"); }
-int vrhip_read_depth8(vrhip_ctx* c, uint8_t* out) { return c ? readback(c, c->depth, out, (size_t)c->W * c->H * 4) : fail(VRHIP_ERR_INVALID, "null ctx"); }
+int vrhip_read_rgba8(vrhip_ctx* c, uint8_t* out)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    const int rc = multi_images(c);
+    return rc ? rc : readback(c, c->rgba, out, (size_t)c->W * c->H * 4);
+}
+int vrhip_read_depth8(vrhip_ctx* c, uint8_t* out)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    const int rc = multi_images(c);
+    return rc ? rc : readback(c, c->depth, out, (size_t)c->W * c->H * 4);
+}
 
 int vrhip_device_buffers(vrhip_ctx* c, void** accum, void** rgba8, void** depth8)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    const int rc = multi_images(c); if (rc) return rc;       // a group's lead: the whole image first
     if (set_device(c) == VRHIP_OK) (void)svc_close(c);     // the buffers hold every render so far
     if (accum) *accum = c->accum;
     if (rgba8) *rgba8 = c->rgba;
@@ -2068,6 +2084,19 @@ static int multi_gather(vrhip_ctx* c, int what)
     return VRHIP_OK;
 }
 
+// The lead's colour and depth images after the last render: the members'
+// render-service sessions close and their RGBA8 and depth tiles are gathered
+// (two grouped ncclGathers), once per run of render calls -- so back-to-back
+// renders with no read in between keep their sessions open across calls.
+static int multi_images(vrhip_ctx* c)
+{
+    if (!c || c->group.empty() || !c->group_stale) return VRHIP_OK;
+    int rc = multi_gather(c, 0);
+    if (rc == VRHIP_OK) rc = multi_gather(c, 2);
+    if (rc == VRHIP_OK) c->group_stale = false;
+    return rc;
+}
+
 int vrhip_create_multi(const int* devices, uint32_t n_devices, uint32_t width, uint32_t height, vrhip_ctx** out)
 {
     if (!out || !devices || n_devices == 0 || n_devices > 64)
@@ -2089,7 +2118,6 @@ int vrhip_create_multi(const int* devices, uint32_t n_devices, uint32_t width, u
     int rc;
     for (uint32_t i = 0; i < n_devices; ++i) {
         if ((rc = vrhip_create(devices[i], width, height, &ms[i])) != VRHIP_OK) return undo(rc);
-        ms[i]->service = 0;               // every render ends with the gather to the lead
         ms[i]->rank = i; ms[i]->nranks = n_devices;
     }
     std::vector<ncclComm_t> comms(n_devices, nullptr);
@@ -2144,25 +2172,26 @@ int vrhip_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
 { return fanout(c, [&](vrhip_ctx* m) { return one_upload_brdf(m, table, n_floats); }); }
 int vrhip_set_overlap(vrhip_ctx* c, int mode) { return fanout(c, [&](vrhip_ctx* m) { return one_set_overlap(m, mode); }); }
 int vrhip_set_path_split(vrhip_ctx* c, uint32_t groups) { return fanout(c, [&](vrhip_ctx* m) { return one_set_path_split(m, groups); }); }
-int vrhip_set_service(vrhip_ctx* c, int mode)
+int vrhip_set_service(vrhip_ctx* c, int mode) { return fanout(c, [&](vrhip_ctx* m) { return one_set_service(m, mode); }); }
+int vrhip_sync(vrhip_ctx* c)
 {
-    if (c && !c->group.empty()) return refuse_multi(c, "vrhip_set_service");
-    return one_set_service(c, mode);
+    const int rc = multi_images(c);                  // a group: the lead's images are complete after a sync
+    return rc ? rc : fanout(c, [&](vrhip_ctx* m) { return one_sync(m); });
 }
-int vrhip_sync(vrhip_ctx* c) { return fanout(c, [&](vrhip_ctx* m) { return one_sync(m); }); }
 
 int vrhip_render(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed)
 {
     if (!c || c->group.empty()) return one_render(c, n_frames, times, time_seed);
-    // every device renders its tiles (asynchronously), then the colour and
-    // depth tiles go to the lead
+    // every device renders its tiles (asynchronously, on its own render
+    // service when calls come back to back); the colour and depth tiles go to
+    // the lead when its images are next needed (multi_images: read-back, GL
+    // present, device buffers, sync)
     for (vrhip_ctx* m : c->group) {
         const int rc = one_render(m, n_frames, times, time_seed);
         if (rc != VRHIP_OK) return rc;
     }
-    int rc = multi_gather(c, 0);
-    if (rc == VRHIP_OK) rc = multi_gather(c, 2);
-    return rc;
+    c->group_stale = true;
+    return VRHIP_OK;
 }
 
 } // extern "C"
