@@ -416,7 +416,9 @@ def main():
             dist.barrier()
         ti = time.perf_counter()
         for i in range(args.interactive_frames):
-            r.render(frames=1, times=[base + 3 + i], sync=True)
+            # one synchronisation per frame, as vRendererCuda::render's
+            # cudaStreamSynchronize (the tile gather, N > 1, is inside it)
+            r.render(frames=1, times=[base + 3 + i], sync=False)
             gather.step()
             r.sync()
         if world > 1:

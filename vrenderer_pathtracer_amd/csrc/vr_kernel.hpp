@@ -1807,9 +1807,21 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         bool ended = false;
         if (state == LS_SHADE) {
             vr4 out;
-            constexpr bool INL = (FEAT & F_INLINE_PRIM) != 0u;   // the path traced its own camera ray
-            if (bounce_step<CNT, FEAT, INL>(p, ray, hr, ps, out, cnt)) {
-                if constexpr (INL) store_path(p, q, slot, out, ps.depth);
+            // one-frame kernels (the path traced its own camera ray) of the
+            // Cornell box and of textured scenes: path 0 of the pixel stores
+            // the depth term at bounce 0 (primary_kernel's formula), so no
+            // register carries it to the path's end -- C3's one-frame kernel
+            // 11 -> 6 spilled VGPRs, C2 one frame per call 0.731 -> 0.722 ms;
+            // the plain HDRI mesh kernel (C5, no spills) keeps it to the end
+            // (1.770 -> 1.790 ms with the early store, r05g)
+            constexpr bool INL = (FEAT & F_INLINE_PRIM) != 0u;
+            constexpr bool EARLY_DEPTH = INL && (FEAT & (F_CORNELL | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
+            if constexpr (EARLY_DEPTH) {
+                if (ps.bounce == 0 && q == 0u)
+                    p.path_w[slot] = hr.t < 1e20f ? depth_term(ray.o, add4(ray.o, mul4s(ray.d, hr.t))) : 1.f;
+            }
+            if (bounce_step<CNT, FEAT, INL && !EARLY_DEPTH>(p, ray, hr, ps, out, cnt)) {
+                if constexpr (INL && !EARLY_DEPTH) store_path(p, q, slot, out, ps.depth);
                 else store_path_rgb(p, q, slot, out);
                 if constexpr ((FEAT & F_SMALL) != 0u) {
                     if (p.path_cost)
