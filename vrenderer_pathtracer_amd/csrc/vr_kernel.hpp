@@ -1534,6 +1534,13 @@ constexpr int path_cache_nodes(int stack, int bt, bool c) {
     return (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * 4) / 56 > 0
                ? (163840 / path_blocks_per_cu(stack, bt, c) - bt - stack * bt * 4) / 56 : 1;
 }
+// The Cornell-box render-service kernels take the 7-wave residency of the
+// Cornell path kernels (r05: with the single refill site and the polynomial
+// constants produced at each use, 4 VGPR spills; C2 whole frames on the
+// service 4,185 -> 4,313 Mpaths/s; at 6 waves they lost 2 % to the launch path)
+#ifndef VR_SVC_CORNELL_RES
+#define VR_SVC_CORNELL_RES 1
+#endif
 template <uint32_t FEAT>
 constexpr bool cornell_kernel() {
     // the one-frame kernels (F_INLINE_PRIM) keep 6 waves: at 7 the interactive
@@ -1541,7 +1548,7 @@ constexpr bool cornell_kernel() {
     // kernels (F_SMALL), which spilled 19 VGPRs at 7 with helper lanes and
     // cost counting (8-rank C2 shard step 1.317 -> 1.257 ms at 6, r03p)
     return (FEAT & F_EXACT) != 0u && (FEAT & F_CORNELL) != 0u && (FEAT & F_INLINE_PRIM) == 0u &&
-           (FEAT & (F_SMALL | F_SERVICE)) == 0u;
+           (FEAT & (F_SMALL | (VR_SVC_CORNELL_RES ? 0u : (uint32_t)F_SERVICE))) == 0u;
 }
 
 #ifndef VR_XCD_BANDS
@@ -2093,9 +2100,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
             __builtin_amdgcn_s_sleep(32);
         }
     };
-    if (!wait_chunk()) return;
-    next = 64u;
-    start(cur_sub, cur_q, cur_L, (uint32_t)lane, cslot);
+    // every lane idle (LS_DONE): the loop's refill waits for the first chunk
     for (;;) {
         if (state == LS_SETUP) {
             if (intersect_spheres<false, FEAT>(p, ray, hr, cnt)) {
@@ -2131,28 +2136,36 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
                 state = LS_SETUP;
             }
         }
-        const unsigned long long em = __ballot(ended);
-        if (em != 0ull) {
-            const uint32_t need = (uint32_t)__popcll(em);
-            uint32_t nsub = ~0u, nq = 0, nL = 0;
-            if (next + need > 64u && cur_sub != ~0u) {
-                ring = grab(nsub, nq, nL, cslot ^ 1u);
-                if (ring != GOT) nsub = ~0u;
+        // refill: lanes whose path ended take the next items; when every
+        // lane is idle the wave waits for the ring's next chunk and all 64
+        // lanes take it (one start() site, so one inlined copy of it)
+        bool take = ended;
+        bool over = false;
+        for (;;) {
+            const unsigned long long em = __ballot(take);
+            if (em != 0ull) {
+                const uint32_t need = (uint32_t)__popcll(em);
+                uint32_t nsub = ~0u, nq = 0, nL = 0;
+                if (next + need > 64u && cur_sub != ~0u) {
+                    ring = grab(nsub, nq, nL, cslot ^ 1u);
+                    if (ring != GOT) nsub = ~0u;
+                }
+                if (take) {
+                    const uint32_t r = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                    const bool here = r < 64u;
+                    start(here ? cur_sub : nsub, here ? cur_q : nq, here ? cur_L : nL, here ? r : r - 64u,
+                          here ? cslot : cslot ^ 1u);
+                }
+                if (next + need > 64u) { cur_sub = nsub; cur_q = nq; cur_L = nL; cslot ^= 1u; next = next + need - 64u; }
+                else next += need;
             }
-            if (ended) {
-                const uint32_t r = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-                if (r < 64u) start(cur_sub, cur_q, cur_L, r, cslot);
-                else start(nsub, nq, nL, r - 64u, cslot ^ 1u);
-            }
-            if (next + need > 64u) { cur_sub = nsub; cur_q = nq; cur_L = nL; cslot ^= 1u; next = next + need - 64u; }
-            else next += need;
+            if (__ballot(state != LS_DONE) != 0ull) break;
+            if (ring == DONE || !wait_chunk()) { over = true; break; }
+            next = 0u;
+            take = true;
         }
-        if (__ballot(state != LS_DONE) == 0ull) {
-            if (ring == DONE || !wait_chunk()) break;
-            next = 64u;
-            start(cur_sub, cur_q, cur_L, (uint32_t)lane, cslot);
-        }
+        if (over) break;
     }
 }
 

@@ -21,7 +21,15 @@ __device__ __forceinline__ double bitsd(uint64_t u) { return __longlong_as_doubl
 // Polynomial constants are materialised into an SGPR pair at each use: gfx9
 // VOP3 has no 64-bit literal, and letting the compiler hoist ~40 of them out
 // of the bounce loop into VGPR pairs costs registers (and occupancy).
-__device__ __forceinline__ double dk(double c) { asm volatile("" : "+s"(c)); return c; }
+template <uint64_t B>
+__device__ __forceinline__ double dk_bits()
+{
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((int32_t)(uint32_t)B));
+    asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((int32_t)(uint32_t)(B >> 32)));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+#define dk(c) dk_bits<__builtin_bit_cast(uint64_t, (double)(c))>()
 
 // ------------------------------------------------------------------ sincos
 __device__ __forceinline__ void sincos_p(float x, float* s, float* c)

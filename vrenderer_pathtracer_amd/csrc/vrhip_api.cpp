@@ -724,6 +724,12 @@ int vrhip_upload_mesh_indexed(vrhip_ctx* c, const float* positions, const float*
 #ifndef VR_SERVICE_HDRI_FRAMES
 #define VR_SERVICE_HDRI_FRAMES 1
 #endif
+// whole frames of Cornell-box mesh scenes on the render service too (its
+// 7-wave Cornell kernel, r05: C2 4,185 -> 4,313 Mpaths/s at 16 frames per
+// step; on the 6-wave kernel of round 4 they lost, 4,111 -> 4,021)
+#ifndef VR_SERVICE_CORNELL_FRAMES
+#define VR_SERVICE_CORNELL_FRAMES 1
+#endif
 
 static int one_upload_hdr(vrhip_ctx* c, const float* rgba, uint32_t w, uint32_t h)
 {
@@ -1351,11 +1357,17 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         const size_t paths_k = (size_t)p.path_stride * 2u * k_max;
         const bool ovl_size = paths_k < ((size_t)1 << 24) || (c->nranks > 1 && paths_k < ((size_t)1 << 25));
         const bool in_flight = c->svc.open || (c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
-        // HDRI mesh scenes take the service for whole frames too: back-to-back
-        // launches then overlap each other's drain (r04 A/B, 16-frame steps, bit-identical:
-        // C3 16,505 -> 18,948, C5 21,630 -> 22,171 Mpaths/s; the Cornell box's
-        // whole frames lose, C2 4,111 -> 4,021, and keep the shard-size limit)
-        const bool svc_size = ovl_size || (VR_SERVICE_HDRI_FRAMES != 0 && !c->cornell);
+        // whole frames take the service too: back-to-back launches then
+        // overlap each other's drain and share one primary pass (r04 A/B,
+        // 16-frame steps, bit-identical: C3 16,505 -> 18,948, C5 21,630 ->
+        // 22,171 Mpaths/s; r05, the 7-wave Cornell service kernel: C2 4,185
+        // -> 4,313)
+        // (Cornell-box scenes with material features run a feature-class
+        // service kernel at 6 waves: C2D's whole frames 3,710 -> 3,687 on it,
+        // so they keep the launch path)
+        const bool c2_exact = f == (vr::F_CORNELL | vr::F_MESH);
+        const bool svc_size = ovl_size || (c->cornell ? (VR_SERVICE_CORNELL_FRAMES != 0 && c2_exact)
+                                                      : VR_SERVICE_HDRI_FRAMES != 0);
         // launches whose slots the scratch budget cannot hold twice take the
         // launch path in every mode (4K frames of many frames per launch)
         const bool svc = count == 0 && wave_kernel && stack <= 32 && n_tiles > 0 &&
