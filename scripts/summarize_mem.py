@@ -30,9 +30,15 @@ CUS = 256
 
 
 def production_wave(name):
-    """The scene's production render kernel: render_wave_kernel (mesh scenes)
-    or render_kernel<16, false, ...> (sphere-only scenes) specialised on the
-    scene's exact feature set (F_EXACT, bit 31), not the counting copies."""
+    """The scene's production render kernel: render_wave_kernel or the
+    render-service kernel (mesh scenes; bench.py's timed steps of C2 / C3 /
+    C5 run in one service dispatch, r05) or render_kernel<16, false, ...>
+    (sphere-only scenes) specialised on the scene's exact feature set
+    (F_EXACT, bit 31), not the counting copies."""
+    m = re.search(r"vr::render_service_kernel<([^>]*)>", name)
+    if m:
+        args = [a.strip() for a in m.group(1).split(",")]
+        return int(args[1].rstrip("u")) >= 2 ** 31
     m = re.search(r"vr::render_wave_kernel<([^>]*)>", name)
     if m:
         args = [a.strip() for a in m.group(1).split(",")]
@@ -58,9 +64,12 @@ def main():
                 per[r["Counter_Name"]].append((int(r["Start_Timestamp"]), float(r["Counter_Value"]),
                                                int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     m, dur = {}, {}
+    svc = any("render_service_kernel" in k for k in kernels)
     for k, v in per.items():
         v.sort()
-        t = v[-TIMED:]
+        # a service run: its timed steps are the last dispatch (one session);
+        # the warmup step before it ran on the launch path
+        t = v[-1:] if svc else v[-TIMED:]
         m[k] = sum(x for _, x, _ in t) / len(t)
         dur[k] = sum(d for _, _, d in t) / len(t)
     lines = [f"# Issue and memory-pipeline counters, {name} ({cfg})", "",

@@ -3,6 +3,7 @@
 // example sphere, its texture maps and the BRDF view tested against the
 // launch's flags): every sphere scene other than C1's and C4's exact feature
 // sets.  Production and instrumented (F_COUNT_EXEC) instantiations.
+#define VR_DK_HOISTED 1      // sphere-only kernels: the hoistable constant form (vr_math.hpp dk)
 #include "vr_kernel.hpp"
 
 namespace vr {

@@ -1822,7 +1822,8 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             // the plain HDRI mesh kernel (C5, no spills) keeps it to the end
             // (1.770 -> 1.790 ms with the early store, r05g)
             constexpr bool INL = (FEAT & F_INLINE_PRIM) != 0u;
-            constexpr bool EARLY_DEPTH = INL && (FEAT & (F_CORNELL | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
+            constexpr bool EARLY_DEPTH = INL && (FEAT & F_EXACT) != 0u &&
+                                         (FEAT & (F_CORNELL | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
             if constexpr (EARLY_DEPTH) {
                 if (ps.bounce == 0 && q == 0u)
                     p.path_w[slot] = hr.t < 1e20f ? depth_term(ray.o, add4(ray.o, mul4s(ray.d, hr.t))) : 1.f;

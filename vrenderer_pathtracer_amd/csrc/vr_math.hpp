@@ -21,6 +21,17 @@ __device__ __forceinline__ double bitsd(uint64_t u) { return __longlong_as_doubl
 // Polynomial constants are materialised into an SGPR pair at each use: gfx9
 // VOP3 has no 64-bit literal, and letting the compiler hoist ~40 of them out
 // of the bounce loop into VGPR pairs costs registers (and occupancy).
+//
+// Two forms.  The path-pool kernels (mesh scenes, bound by the texture
+// path) produce each constant by two s_mov_b32 inside volatile asm at the
+// point of use, so it can neither be hoisted nor kept live in SGPRs across
+// the loop (r05: C2 path kernel SGPR spills 82 -> 41, VGPR spills 2 -> 0,
+// C2 +1.0 %, C3 +0.8 %, C5 +1.4 %).  The sphere-only kernels (C1, C4 and the
+// sphere classes: VALU-bound, no traversal state) keep the round-4 form, an
+// asm that pins an SGPR pair the compiler may materialise once per loop: the
+// per-use s_mov pairs cost them 1-3 % (translation units that define
+// VR_DK_HOISTED before including this header).
+#ifndef VR_DK_HOISTED
 template <uint64_t B>
 __device__ __forceinline__ double dk_bits()
 {
@@ -30,6 +41,9 @@ __device__ __forceinline__ double dk_bits()
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 #define dk(c) dk_bits<__builtin_bit_cast(uint64_t, (double)(c))>()
+#else
+__device__ __forceinline__ double dk(double c) { asm volatile("" : "+s"(c)); return c; }
+#endif
 
 // ------------------------------------------------------------------ sincos
 __device__ __forceinline__ void sincos_p(float x, float* s, float* c)

@@ -1,6 +1,7 @@
 // vr_spec_c4.hip -- the path kernels of scene specialisation C4 (HDRI + MERL BRDF sphere):
 // production and instrumented (F_COUNT_EXEC) instantiations of vr_kernel.hpp.
 // One translation unit per specialisation, so the build compiles them in parallel.
+#define VR_DK_HOISTED 1      // sphere-only kernels: the hoistable constant form (vr_math.hpp dk)
 #include "vr_kernel.hpp"
 
 namespace vr {
