@@ -53,8 +53,12 @@ if {inter} > 0:      # one frame per synchronous call (the reference's render() 
         ti.append((time.perf_counter() - t0) / {inter})
     ti.sort()
     inter = ti[1] * 1e3
+    iacc = r.read_accum()
+    ihash = int(np.bitwise_xor.reduce(iacc.view(np.uint32).reshape(-1)))
+else:
+    ihash = 0
 print(json.dumps({{"mpaths": paths / med / 1e6, "best": paths / ts[0] / 1e6, "inter_ms": inter,
-                   "hash": int(np.bitwise_xor.reduce(acc.view(np.uint32).reshape(-1)))}}))
+                   "hash": int(np.bitwise_xor.reduce(acc.view(np.uint32).reshape(-1))), "ihash": ihash}}))
 """
 
 
@@ -68,12 +72,14 @@ def main():
     ap.add_argument("--node-cost", type=float, default=None, help="SAH node cost of the scene's BVH")
     ap.add_argument("--interactive", type=int, default=0, help="also time N one-frame synchronous calls (median of 3)")
     ap.add_argument("--overlap", default="", help="comma-separated vrhip_set_overlap modes to run per library (1, 0, -1)")
-    ap.add_argument("libs", nargs="+")
+    ap.add_argument("libs", nargs="+", help="lib.so or lib.so@VAR=value,VAR2=value (environment of that run)")
     a = ap.parse_args()
     results = {}
     runs = [(lib, ov) for lib in a.libs for ov in (a.overlap.split(",") if a.overlap else [""])]
-    for lib, ov in runs:
+    for spec, ov in runs:
+        lib, _, envs = spec.partition("@")
         env = dict(os.environ, VRHIP_LIB=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in envs.split(",") if kv)
         if a.leaf:
             env["VRHIP_MAX_LEAF"] = str(a.leaf)
         if a.node_cost is not None:
@@ -87,12 +93,12 @@ def main():
                 sys.exit(p.returncode if p.returncode > 0 else 1)
             continue
         res = json.loads(p.stdout.strip().splitlines()[-1])
-        name = os.path.basename(lib) + (f" overlap={ov}" if ov else "")
+        name = os.path.basename(lib) + (f"@{envs}" if envs else "") + (f" overlap={ov}" if ov else "")
         results[name] = res
         it = f"  one frame/call {res['inter_ms']:.4f} ms" if res.get("inter_ms") else ""
         print(f"{name:40s} {res['mpaths']:9.1f} Mpaths/s (best {res['best']:.1f}){it}  hash {res['hash']:#x}",
               flush=True)
-    hashes = {v["hash"] for v in results.values()}
+    hashes = {(v["hash"], v.get("ihash", 0)) for v in results.values()}
     print("all results identical" if len(hashes) == 1 else f"RESULTS DIFFER: {len(hashes)} distinct hashes")
 
 
