@@ -18,10 +18,13 @@ C2, C3, C5 = E + 9, E + 232, E + 8
 CLS_C, CLS_H = (1 << 30) + 253, (1 << 30) + 252
 rows = [("C2 whole frame", "render_wave_kernel", 16, C2, 256), ("C2 one frame", "render_wave_kernel", 16, C2 + INL + SML, 256),
         ("C2 service", "render_service_kernel", 16, C2 + SVC, 256),
+        ("C2 small shard", "render_wave_kernel", 16, C2 + SML, 256),
         ("C3 whole frame", "render_wave_kernel", 16, C3, 768), ("C3 shard", "render_wave_kernel", 16, C3, 256),
+        ("C3 small shard", "render_wave_kernel", 16, C3 + SML, 256),
         ("C3 one frame", "render_wave_kernel", 16, C3 + INL + SML, 256), ("C3 service", "render_service_kernel", 16, C3 + SVC, 256),
         ("C3 sparse frame", "render_wave_kernel", 16, C3 + SPA, 768), ("C3 sparse service", "render_service_kernel", 16, C3 + SVC + SPA, 256),
         ("C5 whole frame", "render_wave_kernel", 24, C5, 768), ("C5 shard", "render_wave_kernel", 24, C5, 256),
+        ("C5 small shard", "render_wave_kernel", 24, C5 + SML, 256),
         ("C5 one frame", "render_wave_kernel", 24, C5 + INL + SML, 256), ("C5 service", "render_service_kernel", 24, C5 + SVC, 256),
         ("C5 sparse frame", "render_wave_kernel", 24, C5 + SPA, 768), ("C5 sparse service", "render_service_kernel", 24, C5 + SVC + SPA, 256),
         ("class Cornell+mesh", "render_wave_kernel", 16, CLS_C, 768), ("class HDRI+mesh", "render_wave_kernel", 16, CLS_H, 768)]

@@ -179,9 +179,17 @@ struct Hit {                // vHitData, PathTracer.cuh:17-53
     unsigned type;
 };
 
+// A uniform image dimension as a float, converted where it is used: the
+// asm hides the value's loop invariance, so the conversion is not hoisted
+// out of the path loop into a VGPR held across it (the C3 kernels spilled
+// exactly those: float texture heights and the HDRI size)
+__device__ __forceinline__ float dim_f(uint32_t n) {
+    asm volatile("" : "+s"(n));
+    return (float)n;
+}
 __device__ __forceinline__ int tex_addr(uint32_t w, uint32_t h, float u, float v) {
-    const int x = f2i((float)w * u);
-    const int y = f2i((float)h * v);
+    const int x = f2i(dim_f(w) * u);
+    const int y = f2i(dim_f(h) * v);
     const int val = (int)((uint32_t)x + (uint32_t)y * w);
     return (int)clampi(val, 0, (int)(w * h - 1u));
 }
@@ -858,8 +866,11 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
             lx = lx < 0 ? (float)((double)lx + 2.0 * (double)VR_PI) : lx;
             lx = (float)((double)lx / (2.0 * (double)VR_PI));
             ly = ly / VR_PI;
-            const int x = f2i(lx * (float)p.hdr_w);
-            const int y = f2i(ly * (float)p.hdr_h);
+            // (textured kernels: C5's plain HDRI kernels hold the floats
+            // without spilling, and hoisted they cost it nothing)
+            constexpr bool TEX = (FEAT & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
+            const int x = f2i(lx * (TEX ? dim_f(p.hdr_w) : (float)p.hdr_w));
+            const int y = f2i(ly * (TEX ? dim_f(p.hdr_h) : (float)p.hdr_h));
             const int val = (int)((uint32_t)x + (uint32_t)y * p.hdr_w);
             const int addr = (int)clampi(val, 0, (int)(p.hdr_w * p.hdr_h - 1u));
             if (COUNT) { cnt.hdr++; cnt.ld128++; }
@@ -979,7 +990,15 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         ray.o = add4(ray.o, mul4s(normal, 0.05f));
         ray.d = newdir;
     }
-    if (++ps.bounce == 4) {
+    ++ps.bounce;
+    // the production kernels ended the path at bounce 3 above, so only the
+    // reference algorithm reaches a fourth here; the compiler keeps the test
+    // otherwise, and the textured (C3) one-frame kernel spilled the radiance
+    // around it on every bounce.  The untextured kernels keep it: they have
+    // no spill there, and without it C2 lost 0.5 % (code placement) and C5's
+    // one-frame kernel gained a spill.
+    constexpr bool LIVE4 = ref_alg<COUNT, FEAT>() || (FEAT & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) == 0u;
+    if (LIVE4 && ps.bounce == 4) {
         ps.accum.w = ps.depth;
         out = ps.accum;
         return true;
