@@ -1732,6 +1732,15 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     uint32_t next = 64u;                                   // items of the current chunk handed out
     int state = LS_DONE;
     uint32_t q = 0, slot = 0;                              // this lane's path and pixel slot
+    // textured one-frame kernels (C3): the path index -- 0 or 1, one frame --
+    // rides in bit 0 of `slot` (slot << 1 | q): one VGPR less, and the
+    // kernel no longer spills the path's throughput mask in its texture
+    // shading (4 -> 0; the small-shard kernels, packed as slot | q << 24,
+    // only moved theirs).  While a lane helps (help_step), `slot` holds its
+    // owner's lane as everywhere.
+    constexpr bool PACKQ = (FEAT & F_INLINE_PRIM) != 0u && (FEAT & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
+    auto lane_q = [&]() -> uint32_t { return PACKQ ? (slot & 1u) : q; };
+    auto lane_slot = [&]() -> uint32_t { return PACKQ ? (slot >> 1) : slot; };
     uint32_t cam_xy = 0;                                   // F_INLINE_PRIM: its pixel (x << 16 | y) until LS_CAMERA
     Ray ray;
     PathState ps;
@@ -1759,6 +1768,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         if constexpr ((FEAT & F_SMALL) != 0u) cnt.work = 0;
         if constexpr ((FEAT & F_INLINE_PRIM) != 0u) {      // few paths per pixel: trace the camera ray here
             cam_xy = (x << 16) | y;                        // (set up at the top of the loop, out of the refill)
+            if constexpr (PACKQ) slot = (slot << 1) | q;
             state = LS_CAMERA;
             return;
         }
@@ -1844,15 +1854,16 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             constexpr bool EARLY_DEPTH = INL && (FEAT & F_EXACT) != 0u &&
                                          (FEAT & (F_CORNELL | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
             if constexpr (EARLY_DEPTH) {
-                if (ps.bounce == 0 && q == 0u)
-                    p.path_w[slot] = hr.t < 1e20f ? depth_term(ray.o, add4(ray.o, mul4s(ray.d, hr.t))) : 1.f;
+                if (ps.bounce == 0 && lane_q() == 0u)
+                    p.path_w[lane_slot()] = hr.t < 1e20f ? depth_term(ray.o, add4(ray.o, mul4s(ray.d, hr.t))) : 1.f;
             }
             if (bounce_step<CNT, FEAT, INL && !EARLY_DEPTH>(p, ray, hr, ps, out, cnt)) {
-                if constexpr (INL && !EARLY_DEPTH) store_path(p, q, slot, out, ps.depth);
-                else store_path_rgb(p, q, slot, out);
+                if constexpr (INL && !EARLY_DEPTH) store_path(p, lane_q(), lane_slot(), out, ps.depth);
+                else store_path_rgb(p, lane_q(), lane_slot(), out);
                 if constexpr ((FEAT & F_SMALL) != 0u) {
                     if (p.path_cost)
-                        p.path_cost[(size_t)q * p.path_stride + slot] = (uint8_t)(cnt.work < 510u ? cnt.work >> 1 : 255u);
+                        p.path_cost[(size_t)lane_q() * p.path_stride + lane_slot()] =
+                            (uint8_t)(cnt.work < 510u ? cnt.work >> 1 : 255u);
                 }
                 ended = true;
             } else {

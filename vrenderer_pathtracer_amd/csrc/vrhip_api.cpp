@@ -1449,7 +1449,9 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
                               (!wave_kernel && paths_k < ((size_t)1 << 27));
         const bool ovl = count == 0 && (c->overlap > 0 || (c->overlap < 0 && ovl_size && in_flight));
         p.small_blocks = small ? 1u : 0u;
-        p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1) ? 1u : 0u;
+        // (owned pixels < 2^31: the textured one-frame kernels pack the path
+        // index into the pixel slot, vr_kernel.hpp wave_body)
+        p.inline_prim = (2u * k <= (uint32_t)VR_INLINE_PRIM_PATHS && count != 1 && p.path_stride < (1u << 31)) ? 1u : 0u;
         // HDRI mesh launches with a primary pass skip the pixels whose camera
         // ray escapes: one shared result each, the path kernel over the
         // pixels whose camera ray hits (F_SPARSE, vr_kernel.hpp primary_kernel)
