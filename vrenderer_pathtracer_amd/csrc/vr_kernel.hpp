@@ -854,9 +854,12 @@ __device__ __forceinline__ void probe_coherent(float& rand1, float& rand2)
 // One bounce of trace's loop body (:627-769) for the closest hit `hr` of
 // `ray` (hr.t == 1e20: miss).  Returns true when the path ends, with its
 // radiance (w = depth) in `out`; otherwise `ray` is the next bounce's ray.
-template <bool COUNT, uint32_t FEAT, bool DEPTH = true>
+// bounce_step's exits call `sink` with the path's result (the render
+// service's store at each exit; the default stores nothing)
+struct NoSink { __device__ __forceinline__ void operator()(const vr4&) const {} };
+template <bool COUNT, uint32_t FEAT, bool DEPTH = true, typename Sink = NoSink>
 __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, const HitRec& hr, PathState& ps,
-                                            vr4& out, Cnt& cnt)
+                                            vr4& out, Cnt& cnt, const Sink& sink = Sink())
 {
     const bool hit = hr.t < 1e20f;
     if (!hit) {
@@ -877,6 +880,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
             ps.accum = add4(ps.accum, mul4(mul4s(ps.mask, 2.f), p.hdr[addr]));
             ps.accum.w = ps.depth;
             out = ps.accum;
+            sink(out);
             return true;
         }
         // Cornell escape (:649-650): radiance and .w are 0.  The x channel
@@ -885,6 +889,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         // leaves its bits unchanged) -- and marks the escape in the
         // path-result scratch, which does not store .w (store_path).
         out = mk4(-0.f, 0.f, 0.f, 0.f);
+        sink(out);
         return true;
     }
     if (!ref_alg<COUNT, FEAT>() && ps.bounce == 3) {
@@ -893,6 +898,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         ps.accum = add4(ps.accum, mul4(ps.mask, emission_of(hr)));
         ps.accum.w = ps.depth;
         out = ps.accum;
+        sink(out);
         return true;
     }
     Hit h;
@@ -1001,6 +1007,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
     if (LIVE4 && ps.bounce == 4) {
         ps.accum.w = ps.depth;
         out = ps.accum;
+        sink(out);
         return true;
     }
     return false;
@@ -2160,12 +2167,23 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
         bool ended = false;
         if (state == LS_SHADE) {
             vr4 out;
-            if (bounce_step<false, FEAT, false>(p, ray, hr, ps, out, cnt)) {
-                svc_store_path(p, q >> 8, q & 0xffu, slot, out);
-                ended = true;
+            // Cornell-box and textured kernels store the result at each of
+            // bounce_step's exits: stored after the join, the merged radiance
+            // was spilled around it -- three scratch loads on every bounce of
+            // C2's service kernel (6 spills -> 0, C2 +0.5 %, C3 +1 %); the
+            // plain HDRI kernels (C5, no spills) keep the join (-0.4 % without)
+            constexpr bool AT_EXIT = (FEAT & (F_CORNELL | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
+            bool done;
+            if constexpr (AT_EXIT) {
+                done = bounce_step<false, FEAT, false>(p, ray, hr, ps, out, cnt, [&](const vr4& o) {
+                    svc_store_path(p, q >> 8, q & 0xffu, slot, o);
+                });
             } else {
-                state = LS_SETUP;
+                done = bounce_step<false, FEAT, false>(p, ray, hr, ps, out, cnt);
+                if (done) svc_store_path(p, q >> 8, q & 0xffu, slot, out);
             }
+            if (done) ended = true;
+            else state = LS_SETUP;
         }
         // refill: lanes whose path ended take the next items; when every
         // lane is idle the wave waits for the ring's next chunk and all 64
