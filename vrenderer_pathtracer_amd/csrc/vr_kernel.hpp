@@ -1864,7 +1864,22 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 if (ps.bounce == 0 && lane_q() == 0u)
                     p.path_w[lane_slot()] = hr.t < 1e20f ? depth_term(ray.o, add4(ray.o, mul4s(ray.d, hr.t))) : 1.f;
             }
-            if (bounce_step<CNT, FEAT, INL && !EARLY_DEPTH>(p, ray, hr, ps, out, cnt)) {
+            // the plain HDRI small-launch kernels (C5 shards) store at each
+            // exit of the bounce step (2 spills -> 0 there; elsewhere the
+            // join form compiles spill-free or better)
+            constexpr bool AT_EXIT = (FEAT & F_SMALL) != 0u && !INL &&
+                                     (FEAT & (F_CORNELL | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) == 0u;
+            if constexpr (AT_EXIT) {
+                if (bounce_step<CNT, FEAT, false>(p, ray, hr, ps, out, cnt, [&](const vr4& o) {
+                        store_path_rgb(p, q, slot, o);
+                        if (p.path_cost)
+                            p.path_cost[(size_t)q * p.path_stride + slot] = (uint8_t)(cnt.work < 510u ? cnt.work >> 1 : 255u);
+                    })) {
+                    ended = true;
+                } else {
+                    state = LS_SETUP;
+                }
+            } else if (bounce_step<CNT, FEAT, INL && !EARLY_DEPTH>(p, ray, hr, ps, out, cnt)) {
                 if constexpr (INL && !EARLY_DEPTH) store_path(p, lane_q(), lane_slot(), out, ps.depth);
                 else store_path_rgb(p, lane_q(), lane_slot(), out);
                 if constexpr ((FEAT & F_SMALL) != 0u) {
