@@ -649,6 +649,16 @@ __device__ __forceinline__ bool intersect_scene(const RenderParams& p, const Ray
 
 // Materialise vHitData for the final hit (the values the reference's last
 // accepted hit wrote; :160-168, :180-189, :198-266, :380-453).
+// Face normals from the traversal's triangle edges (fill_hit): on in every
+// kernel but the Cornell-box one-frame kernels, which spill 2 VGPRs with it
+// (C2 16-frame steps +0.7 %, C5 one frame per call -1 %, r05s)
+#ifndef VR_FACE_FROM_EDGES
+#define VR_FACE_FROM_EDGES 1
+#endif
+template <uint32_t FEAT>
+constexpr bool face_from_edges() {
+    return VR_FACE_FROM_EDGES != 0 && !((FEAT & F_INLINE_PRIM) != 0u && (FEAT & F_CORNELL) != 0u);
+}
 template <uint32_t FEAT>
 __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, const HitRec& hr, Hit& h)
 {
@@ -714,6 +724,20 @@ __device__ __forceinline__ void fill_hit(const RenderParams& p, const Ray& r, co
             const vr4 bitangent = cross4(normal, tangent);
             const vr4 nm = normalize4(sub4(muls4(2.f, p.tex[1][ta]), mk4(1.f, 1.f, 1.f, 0.f)));
             h.n = normalize4(tbn_mul(tangent, bitangent, normal, nm));
+        } else if constexpr (face_from_edges<FEAT>()) {
+            // the face normal from the traversal's copy of the triangle, whose
+            // lines the leaf loop just fetched (L1 / L2-hot, 24 B instead of
+            // the 36 B of p.verts): its edges e1 = v1 - v0, e2 = v2 - v0 were
+            // rounded at upload as the reference's v0 - v1, v0 - v2 negated
+            // (IEEE subtraction is sign-symmetric), and the cross product of
+            // two negated vectors is the same bits -- the same normal
+            const __amdgpu_buffer_rsrc_t tbuf = buf_rsrc(p.tri_e, p.n_tris * 36u);
+            const int o = (a / 3) * 36;
+            const vr_u32x3 q1 = __builtin_amdgcn_raw_buffer_load_b96(tbuf, o + 12, 0, 0);
+            const vr_u32x3 q2 = __builtin_amdgcn_raw_buffer_load_b96(tbuf, o + 24, 0, 0);
+            const vr4 e1 = mk4(__uint_as_float(q1.x), __uint_as_float(q1.y), __uint_as_float(q1.z), 0.f);
+            const vr4 e2 = mk4(__uint_as_float(q2.x), __uint_as_float(q2.y), __uint_as_float(q2.z), 0.f);
+            h.n = normalize4(cross4(e1, e2));
         } else {
             const vr3 a0 = p.verts[a], a1 = p.verts[a + 1], a2 = p.verts[a + 2];
             const vr4 v0 = mk4(a0.x, a0.y, a0.z, 0.f), v1 = mk4(a1.x, a1.y, a1.z, 0.f), v2 = mk4(a2.x, a2.y, a2.z, 0.f);
@@ -901,8 +925,35 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         sink(out);
         return true;
     }
+    // The diffuse branch's direction sample (the two draws after the Fresnel
+    // draw, sincos of the azimuth, the two square roots) computed before the
+    // material is known, from a copy of the generator: it depends on the
+    // generator alone, so it interleaves with the hit's normal / Fresnel
+    // chain instead of trailing it; committed only when the bounce takes that
+    // branch.  VR_SPEC_SAMPLE 2: before fill_hit, 1: after it, 0: off.  On in
+    // the Cornell-box service and one-frame kernels, whose bounces are almost
+    // all diffuse (C2 16-frame steps +0.5 %, one frame per call 0.718 ->
+    // 0.714 ms, r05s); the HDRI kernels spilled with it (C3 one frame +1 %)
+    // and the 7-wave whole-frame kernel spilled 4 VGPRs.
+#ifndef VR_SPEC_SAMPLE
+#define VR_SPEC_SAMPLE 2
+#endif
+    constexpr bool SPEC = VR_SPEC_SAMPLE != 0 && !ref_alg<COUNT, FEAT>() && (FEAT & (F_BRDF | F_VIEW_BRDF)) == 0u &&
+                          (FEAT & F_CORNELL) != 0u && (FEAT & (F_SERVICE | F_INLINE_PRIM)) != 0u;
+    Rng srng = ps.rng;
+    float su0 = 0.f, srand2s = 0.f, srand1m = 0.f, ssn = 0.f, scs = 0.f;
+    auto spec_sample = [&]() {
+        su0 = srng.uniform();
+        const float rand1 = 2.f * VR_PI * srng.uniform();
+        const float rand2 = srng.uniform();
+        srand2s = sqrt_exact(rand2);
+        srand1m = sqrt_exact(1 - rand2);
+        sincos_p(rand1, &ssn, &scs);
+    };
+    if constexpr (SPEC && VR_SPEC_SAMPLE == 2) spec_sample();
     Hit h;
     fill_hit<FEAT>(p, ray, hr, h);
+    if constexpr (SPEC && VR_SPEC_SAMPLE == 1) spec_sample();
     if (COUNT) {
         if (hr.kind == HK_MESH) {
             cnt.attr += 24 + 48;
@@ -920,8 +971,10 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
                 cnt.attr += 48; cnt.tex++; cnt.nmap_hits++;
                 cnt.ld128 += 3 + 1;                            // normals + the normal-map texel
             } else if (!ref_alg<COUNT, FEAT>()) {
-                cnt.attr += 36;     // the face normal's vertices (the reference has them from its triangle test)
-                cnt.ld96 += 3;
+                // the face normal's edges (face_from_edges) or vertices (the
+                // reference has them from its triangle test)
+                cnt.attr += face_from_edges<FEAT>() ? 24 : 36;
+                cnt.ld96 += face_from_edges<FEAT>() ? 2 : 3;
             }
         } else if (hr.kind == HK_EXAMPLE) {
             const bool vb = HAS(F_VIEW_BRDF);
@@ -944,13 +997,23 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
         float fe = 0.f;
         if (h.spec.x != 0.f)
             fe = ((1.f - p.fresnel_coef) * pow_p(1.f - aoi, p.fresnel_pow) + p.fresnel_coef * 1.f) * h.spec.x;
-        const bool reflect = (ps.rng.uniform() < fe);
+        const bool reflect = ((SPEC ? su0 : ps.rng.uniform()) < fe);
         vr4 newdir;
         const vr4 w = normal;
         const vr4 axis = __builtin_fabsf(w.x) > 0.1f ? mk4(0.f, 1.f, 0.f, 0.f) : mk4(1.f, 0.f, 0.f, 0.f);
         if (reflect) {
+            if constexpr (SPEC) (void)ps.rng.uniform();        // the Fresnel draw only
             muleq4(ps.mask, h.spec);
             newdir = normalize4(sub4(ray.d, mul4s(mul4s(normal, 2.f), dot4(normal, ray.d))));
+        } else if constexpr (SPEC) {
+            ps.rng = srng;                                      // the three draws
+            const vr4 u = normalize4(cross4(axis, w));
+            const vr4 v = cross4(w, u);
+            newdir = normalize4(add4(add4(mul4s(mul4s(u, scs), srand2s), mul4s(mul4s(v, ssn), srand2s)),
+                                     mul4s(w, srand1m)));
+            muleq4(ps.mask, h.col);
+            muleq4s(ps.mask, dot4(newdir, normal));
+            muleq4s(ps.mask, 2.f);
         } else {
             float rand1 = 2.f * VR_PI * ps.rng.uniform();
             float rand2 = ps.rng.uniform();
