@@ -407,6 +407,9 @@ def main():
     inter = None
     if args.interactive_frames > 0:
         r.clearBuffer()
+        # the Qt adapter's configuration (integration/vRendererHIP.cpp): no
+        # kernel-timing events on the launch path (nothing reads them there)
+        r.set_kernel_timing(False)
         base = scene["time"] + 100000
         for i in range(3):
             r.render(frames=1, times=[base + i], sync=True)
@@ -427,12 +430,14 @@ def main():
         if world > 1:
             dist.all_reduce(te, op=dist.ReduceOp.MAX)
         te = float(te.item())
+        r.set_kernel_timing(True)
         pf = (W // 16) * 16 * (H // 16) * 16 * 2
         inter = {"frames_per_step": 1, "frames": args.interactive_frames,
                  "value": round(pf * args.interactive_frames / te / 1e6, 3), "unit": "Mpaths/s",
                  "ms_per_frame": round(te / args.interactive_frames * 1e3, 4),
                  "note": "one frame per synchronous render() call (src/vRendererCuda.cpp:107-165 syncs every "
-                         "frame)" + (", plus the RGBA8 tile gather to rank 0 per frame" if world > 1 else "")}
+                         "frame)" + (", plus the RGBA8 tile gather to rank 0 per frame" if world > 1 else "")
+                 + "; kernel-timing events off, as in the Qt adapter (vrhip_set_kernel_timing)"}
 
     # aggregate counts over ranks
     keys = sorted(ref_counts)

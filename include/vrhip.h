@@ -328,9 +328,18 @@ int vrhip_comm_destroy(vrhip_ctx *ctx);
 
 /* ---- diagnostics ------------------------------------------------------ */
 /* Kernel time of the last vrhip_render (ms, HIP events on the context stream;
- * requires vrhip_sync first).  After a render-service session: the session's
- * span, from its kernel's start to its finish pass's end (all its launches). */
+ * requires vrhip_sync first; 0 with kernel timing off).  After a
+ * render-service session: the session's span, from its kernel's start to its
+ * finish pass's end (all its launches). */
 int vrhip_last_kernel_ms(vrhip_ctx *ctx, float *ms);
+/* Kernel timing (diagnostics; no reference counterpart): on (default; also
+ * VRHIP_KERNEL_TIMING=1) the library records HIP events around each call and
+ * around every launch's render kernels for vrhip_last_kernel_ms and
+ * vrhip_kernel_stats; off, it records none on the launch path -- they sit
+ * between the kernels on the stream and cost about 8 µs per synchronous
+ * one-frame call (C2 0.712 -> 0.704 ms per frame), so a host at the
+ * reference's one-frame cadence that does not read them turns them off. */
+int vrhip_set_kernel_timing(vrhip_ctx *ctx, int on);
 /* Accumulated render-kernel time (ms) and launch count since the last reset,
  * from HIP events recorded around every launch's render kernels
  * (primary_kernel + render_wave_kernel, or render_kernel) on the stream they

@@ -93,6 +93,9 @@ void vRendererHIP::init(const unsigned int &_w, const unsigned int &_h)
     validate(vrhip_create(devices.size() == 1 ? devices[0] : (dev ? std::atoi(dev) : 0), _w, _h, &m_ctx),
              "Create HIP context");
   }
+  // no kernel-timing events on the launch path: nothing here reads them, and
+  // at one synchronous frame per paint they cost ~8 us a frame
+  validate(vrhip_set_kernel_timing(m_ctx, 0), "Kernel timing off");
   validate(vrhip_set_fresnel(m_ctx, m_fresnelCoef, m_fresnelPow), "Set Fresnel parameters");
   m_rgba.assign(static_cast<size_t>(_w) * _h * 4, 0);
   m_depth.assign(static_cast<size_t>(_w) * _h * 4, 0);

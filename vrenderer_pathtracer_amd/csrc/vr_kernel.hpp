@@ -938,8 +938,12 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
 #ifndef VR_SPEC_SAMPLE
 #define VR_SPEC_SAMPLE 2
 #endif
+#ifndef VR_SPEC_HDRI_SVC
+#define VR_SPEC_HDRI_SVC 0
+#endif
     constexpr bool SPEC = VR_SPEC_SAMPLE != 0 && !ref_alg<COUNT, FEAT>() && (FEAT & (F_BRDF | F_VIEW_BRDF)) == 0u &&
-                          (FEAT & F_CORNELL) != 0u && (FEAT & (F_SERVICE | F_INLINE_PRIM)) != 0u;
+                          (((FEAT & F_CORNELL) != 0u && (FEAT & (F_SERVICE | F_INLINE_PRIM)) != 0u) ||
+                           (VR_SPEC_HDRI_SVC != 0 && (FEAT & F_SERVICE) != 0u));
     Rng srng = ps.rng;
     float su0 = 0.f, srand2s = 0.f, srand1m = 0.f, ssn = 0.f, scs = 0.f;
     auto spec_sample = [&]() {

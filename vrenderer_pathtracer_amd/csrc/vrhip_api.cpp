@@ -135,7 +135,12 @@ struct vrhip_ctx {
     struct Span { hipEvent_t first, second; uint32_t launches; };
     std::deque<Span> kev_pending;
     std::vector<hipEvent_t> kev_free;
-    bool timed = false;          // ev0/ev1 hold the last render
+    bool timed = false;          // ev1 marks the end of the last render
+    bool ev0_valid = false;      // ev0 marks its start (kernel timing on)
+    // vrhip_set_kernel_timing (VRHIP_KERNEL_TIMING=0: off): span events around
+    // every launch's render kernels (vrhip_kernel_stats) and each call
+    // (vrhip_last_kernel_ms)
+    bool kernel_timing = true;
     double kernel_ms_total = 0.0;    // union of the launches' render-kernel spans (overlapping launches count once)
     uint64_t launches_total = 0;
     uint32_t last_split = 1, last_use_scratch = 0, last_kind = 0;   // vrhip_last_launch_info
@@ -543,6 +548,7 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     c->W = width; c->H = height;
     c->fov_scale = default_fov_scale();
     if (const char* e = std::getenv("VRHIP_COST_ORDER")) c->cost_order = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VRHIP_KERNEL_TIMING")) c->kernel_timing = std::atoi(e) != 0;
     if (const char* e = std::getenv("VRHIP_SERVICE")) c->service = std::max(-1, std::min(1, std::atoi(e)));
     int rc;
     if ((rc = set_device(c)) != VRHIP_OK) { delete c; return rc; }
@@ -1237,6 +1243,7 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     HIP_TRY(hipMemsetAsync(S.qctl, 0, (size_t)slots * vr::kSvcQctlWords * 4u, S.s));
     HIP_TRY(hipEventRecord(S.k0, S.s));
     HIP_TRY(hipEventRecord(c->ev0, S.s));
+    c->ev0_valid = true;
     const int e = vr::launch_service(S.p, n_tiles, stack, S.s);
     if (e != 0) return fail(VRHIP_ERR_HIP, std::string("service launch: ") + hipGetErrorString((hipError_t)e));
     HIP_TRY(hipEventRecord(S.k1, S.s));
@@ -1407,7 +1414,8 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             }
         }
     }
-    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    if (c->kernel_timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    c->ev0_valid = c->kernel_timing;
     while (done < n_frames) {
         const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
         p.first_frame = c->frame;
@@ -1510,7 +1518,10 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             if (l.order_pending) { HIP_TRY(hipStreamWaitEvent(rs, l.ordered, 0)); l.order_pending = false; }
         }
         hipEvent_t k0 = nullptr, k1 = nullptr;
-        if (n_tiles) {
+        // per-launch span events (vrhip_kernel_stats) only with kernel timing
+        // on (vrhip_set_kernel_timing): recorded on the stream around the
+        // render kernels they cost ≈ 8 µs per synchronous one-frame call
+        if (n_tiles && c->kernel_timing) {
             if ((rc = take_event(c, &k0)) != VRHIP_OK || (rc = take_event(c, &k1)) != VRHIP_OK) return rc;
             c->kev_pending.push_back({ k0, k1, 1u });
             HIP_TRY(hipEventRecord(k0, rs));
@@ -1521,7 +1532,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         }
         int e = vr::launch_render(p, n_tiles, stack, count, rs);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
-        if (n_tiles) HIP_TRY(hipEventRecord(k1, rs));
+        if (k1) HIP_TRY(hipEventRecord(k1, rs));
         if (on_lane) {
             HIP_TRY(hipEventRecord(l.done, rs));
             HIP_TRY(hipStreamWaitEvent(c->stream, l.done, 0));
@@ -1938,9 +1949,16 @@ int vrhip_last_kernel_ms(vrhip_ctx* c, float* ms)
 {
     if (!c || !ms) return fail(VRHIP_ERR_INVALID, "null argument");
     if (set_device(c) == VRHIP_OK) (void)svc_close(c);
-    if (!c->timed) { *ms = 0.f; return VRHIP_OK; }
+    if (!c->timed || !c->ev0_valid) { *ms = 0.f; return VRHIP_OK; }   // no render, or kernel timing off
     HIP_TRY(hipEventSynchronize(c->ev1));
     HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return VRHIP_OK;
+}
+
+static int one_set_kernel_timing(vrhip_ctx* c, int on)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    c->kernel_timing = on != 0;
     return VRHIP_OK;
 }
 
@@ -2187,6 +2205,7 @@ int vrhip_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
 int vrhip_set_overlap(vrhip_ctx* c, int mode) { return fanout(c, [&](vrhip_ctx* m) { return one_set_overlap(m, mode); }); }
 int vrhip_set_path_split(vrhip_ctx* c, uint32_t groups) { return fanout(c, [&](vrhip_ctx* m) { return one_set_path_split(m, groups); }); }
 int vrhip_set_service(vrhip_ctx* c, int mode) { return fanout(c, [&](vrhip_ctx* m) { return one_set_service(m, mode); }); }
+int vrhip_set_kernel_timing(vrhip_ctx* c, int on) { return fanout(c, [&](vrhip_ctx* m) { return one_set_kernel_timing(m, on); }); }
 int vrhip_sync(vrhip_ctx* c)
 {
     const int rc = multi_images(c);                  // a group: the lead's images are complete after a sync

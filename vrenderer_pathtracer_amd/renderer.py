@@ -359,6 +359,12 @@ class VRendererHIP:
         kernel): 1 always, 0 never, -1 automatic (vrhip_set_service)."""
         check(self._lib.vrhip_set_service(self._need_ctx(), int(mode)), "vrhip_set_service")
 
+    def set_kernel_timing(self, on: bool) -> None:
+        """HIP events around calls and launches for kernel_stats /
+        last_kernel_ms (vrhip_set_kernel_timing; off saves ~8 us per
+        synchronous one-frame call)."""
+        check(self._lib.vrhip_set_kernel_timing(self._need_ctx(), int(bool(on))), "vrhip_set_kernel_timing")
+
     def set_service_timing(self, idle_us: int = 0, post_window_us: int = 0, post_delay_us: int = 0) -> None:
         """Test hook (vrhip_set_service_timing): the session kernel's idle
         limit, the host's post window and a host delay before each post
