@@ -108,18 +108,24 @@ struct vrhip_ctx {
         vr4* prim = nullptr;         // primary hits, 2 float4 per owned pixel
         size_t prim_cap = 0;         // float4 elements
         uint32_t* chunk_ctr = nullptr;   // wave kernel work queue heads
-        // longest-first scheduling: per sub-tile costs measured by the last
-        // launch on this scratch and the per-XCD order sorted from them
-        uint32_t* sub_cost = nullptr;
-        uint32_t* sub_order = nullptr;
+        // longest-first scheduling: per sub-tile costs measured by a launch
+        // on this scratch and the per-XCD order sorted from them, in two
+        // slots used by turns (ordered launch i measures into slot oi and
+        // takes the order launch i-2 left there: its sort is long finished,
+        // so the launch waits for nothing -- with one slot, a one-frame
+        // call's launch waited for the sort of the call before, ≈ 12 µs of
+        // cross-stream hand-off per synchronous frame, r05)
+        uint32_t* sub_cost[2] = { nullptr, nullptr };
+        uint32_t* sub_order[2] = { nullptr, nullptr };
         size_t sub_cap = 0;          // sub-tiles the buffers hold
-        uint32_t order_nsub = 0;     // sub-tile count the order was sorted for (0: none)
+        uint32_t order_nsub[2] = { 0, 0 };   // sub-tile count each slot's order was sorted for (0: none)
+        uint32_t oi = 0;             // the slot the next ordered launch uses
         uint32_t* px_list = nullptr;     // F_SPARSE launches: the pixels whose camera ray hits (RenderParams::sparse_px)
         size_t px_cap = 0;
         hipEvent_t done = nullptr;   // recorded on `s` after the render kernels
         hipEvent_t finished = nullptr;   // recorded on `stream` after the finish pass that read this scratch
-        hipEvent_t ordered = nullptr;    // recorded on `s` after the order pass sorting this scratch's costs
-        bool order_pending = false;      // an order pass was queued since this scratch's last launch
+        hipEvent_t ordered[2] = { nullptr, nullptr };   // recorded on `s` after the order pass of each slot
+        bool order_pending[2] = { false, false };       // an order pass was queued on the slot since a launch waited for it
         bool used = false;
     } lane[VR_PATH_STREAMS];
     uint32_t parity = 0;
@@ -560,7 +566,8 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
         if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&l.finished, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&l.ordered, hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&l.ordered[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&l.ordered[1], hipEventDisableTiming) != hipSuccess)
             return cleanup(fail(VRHIP_ERR_HIP, "path stream setup failed"));
     }
     if (hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
@@ -618,9 +625,11 @@ int vrhip_destroy(vrhip_ctx* c)
     if (c->comm) (void)ncclCommDestroy(c->comm);
     dfree(c->comm_send); dfree(c->comm_recv);
     for (auto& l : c->lane) {
-        dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr); dfree(l.sub_cost); dfree(l.sub_order); dfree(l.px_list);
+        dfree(l.paths); dfree(l.prim); dfree(l.chunk_ctr); dfree(l.px_list);
+        for (int i = 0; i < 2; ++i) { dfree(l.sub_cost[i]); dfree(l.sub_order[i]); }
         if (l.done) (void)hipEventDestroy(l.done);
-        if (l.ordered) (void)hipEventDestroy(l.ordered);
+        for (int i = 0; i < 2; ++i)
+            if (l.ordered[i]) (void)hipEventDestroy(l.ordered[i]);
         if (l.finished) (void)hipEventDestroy(l.finished);
         if (l.s) (void)hipStreamDestroy(l.s);
     }
@@ -1000,10 +1009,13 @@ static int ensure_lane(vrhip_ctx* c, vrhip_ctx::Lane& l, size_t need, uint32_t p
         l.px_cap = path_stride;
     }
     if (n_sub > l.sub_cap) {                              // the order buffers hold 8 XCD lists of order_cap(n_sub)
-        dfree(l.sub_cost); dfree(l.sub_order);
-        l.sub_cap = 0; l.order_nsub = 0;
-        HIP_TRY(hipMalloc((void**)&l.sub_cost, n_sub * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc((void**)&l.sub_order, 8u * order_cap(n_sub) * sizeof(uint32_t)));
+        l.sub_cap = 0;
+        for (int i = 0; i < 2; ++i) {
+            dfree(l.sub_cost[i]); dfree(l.sub_order[i]);
+            l.order_nsub[i] = 0;
+            HIP_TRY(hipMalloc((void**)&l.sub_cost[i], n_sub * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc((void**)&l.sub_order[i], 8u * order_cap(n_sub) * sizeof(uint32_t)));
+        }
         l.sub_cap = n_sub;
     }
     if (!l.chunk_ctr) {
@@ -1509,13 +1521,25 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             // per-path costs after the radiances and depth terms in the scratch
             // (need x 16 B holds need x 12 + path_stride x 4 + need x 1)
             p.path_cost = order ? reinterpret_cast<uint8_t*>(p.path_w + p.path_stride) : nullptr;
-            p.sub_cost = order ? l.sub_cost : nullptr;
-            p.sub_order = (order && l.order_nsub == n_sub) ? l.sub_order : nullptr;
+            // VRHIP_ORDER_SLOTS=1 (measurement): one slot, the previous launch's order
+            static const uint32_t order_slots = [] {
+                const char* e = std::getenv("VRHIP_ORDER_SLOTS");
+                return (e && std::atoi(e) == 1) ? 1u : 2u;
+            }();
+            const uint32_t w = order_slots == 2u ? l.oi : 0u;
+            p.sub_cost = order ? l.sub_cost[w] : nullptr;
+            p.sub_order = (order && l.order_nsub[w] == n_sub) ? l.sub_order[w] : nullptr;
             p.order_cap = (uint32_t)order_cap(n_sub);
             if (on_lane && l.used) HIP_TRY(hipStreamWaitEvent(rs, l.finished, 0));
-            // the last order pass on this scratch (it read sub_cost, which this
-            // launch's finish pass rewrites, and wrote the order this launch reads)
-            if (l.order_pending) { HIP_TRY(hipStreamWaitEvent(rs, l.ordered, 0)); l.order_pending = false; }
+            // the order pass of this slot (it read the slot's costs, which this
+            // launch's finish pass rewrites, and wrote the order this launch
+            // reads); a launch that does not order waits for both slots
+            for (uint32_t i = 0; i < 2u; ++i) {
+                if ((i == w || !order) && l.order_pending[i]) {
+                    HIP_TRY(hipStreamWaitEvent(rs, l.ordered[i], 0));
+                    l.order_pending[i] = false;
+                }
+            }
         }
         hipEvent_t k0 = nullptr, k1 = nullptr;
         // per-launch span events (vrhip_kernel_stats) only with kernel timing
@@ -1544,17 +1568,18 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             l.used = true;
         }
         if (p.path_cost) {
-            // the next launch on this scratch takes this launch's order: sorted
-            // on the path stream behind this finish pass, off the context
-            // stream, so a synchronous caller does not wait for it (one frame
-            // per call: it runs in the host's gap before the next launch,
-            // which waits for it)
+            // the next launch but one on this scratch takes this launch's
+            // order (the slots alternate): sorted on the path stream behind
+            // this finish pass, off the context stream, so a synchronous
+            // caller waits for it neither here nor at its next launch
+            const uint32_t w = p.sub_cost == l.sub_cost[0] ? 0u : 1u;
             HIP_TRY(hipStreamWaitEvent(l.s, l.finished, 0));
-            e = vr::launch_order(p.sub_cost, l.sub_order, p.path_stride / 64u, p.order_cap, l.s);
+            e = vr::launch_order(p.sub_cost, l.sub_order[w], p.path_stride / 64u, p.order_cap, l.s);
             if (e != 0) return fail(VRHIP_ERR_HIP, std::string("order launch: ") + hipGetErrorString((hipError_t)e));
-            HIP_TRY(hipEventRecord(l.ordered, l.s));
-            l.order_pending = true;
-            l.order_nsub = p.path_stride / 64u;
+            HIP_TRY(hipEventRecord(l.ordered[w], l.s));
+            l.order_pending[w] = true;
+            l.order_nsub[w] = p.path_stride / 64u;
+            l.oi = w ^ 1u;
         }
         c->frame += k;
         done += k;
