@@ -941,8 +941,14 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
 #ifndef VR_SPEC_HDRI_SVC
 #define VR_SPEC_HDRI_SVC 0
 #endif
+// (also measured, off: the HDRI service kernels -- C3 -0.4 %, C5 +0.3 %,
+// noise -- and the Cornell whole-frame kernel: ±0, r05v)
+#ifndef VR_SPEC_WHOLE
+#define VR_SPEC_WHOLE 0
+#endif
     constexpr bool SPEC = VR_SPEC_SAMPLE != 0 && !ref_alg<COUNT, FEAT>() && (FEAT & (F_BRDF | F_VIEW_BRDF)) == 0u &&
-                          (((FEAT & F_CORNELL) != 0u && (FEAT & (F_SERVICE | F_INLINE_PRIM)) != 0u) ||
+                          (((FEAT & F_CORNELL) != 0u &&
+                            ((FEAT & (F_SERVICE | F_INLINE_PRIM)) != 0u || (VR_SPEC_WHOLE != 0 && (FEAT & F_SMALL) == 0u))) ||
                            (VR_SPEC_HDRI_SVC != 0 && (FEAT & F_SERVICE) != 0u));
     Rng srng = ps.rng;
     float su0 = 0.f, srand2s = 0.f, srand1m = 0.f, ssn = 0.f, scs = 0.f;
@@ -1931,16 +1937,30 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 if (ps.bounce == 0 && lane_q() == 0u)
                     p.path_w[lane_slot()] = hr.t < 1e20f ? depth_term(ray.o, add4(ray.o, mul4s(ray.d, hr.t))) : 1.f;
             }
-            // the plain HDRI small-launch kernels (C5 shards) store at each
-            // exit of the bounce step (2 spills -> 0 there; elsewhere the
-            // join form compiles spill-free or better)
-            constexpr bool AT_EXIT = (FEAT & F_SMALL) != 0u && !INL &&
-                                     (FEAT & (F_CORNELL | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) == 0u;
+            // Stores at each exit of the bounce step (bit 1: the plain HDRI
+            // small-launch kernels, C5 shards: 2 spills -> 0; bit 2: the
+            // Cornell whole-frame kernels, C2 without the service +0.3 %;
+            // bit 4: the Cornell one-frame kernels, measured +0.5 % per
+            // synchronous frame, off); elsewhere the join form compiles
+            // spill-free or better (r05v)
+#ifndef VR_WAVE_AT_EXIT
+#define VR_WAVE_AT_EXIT 3
+#endif
+            constexpr bool CORN = (FEAT & F_CORNELL) != 0u;
+            constexpr bool AT_EXIT =
+                ((VR_WAVE_AT_EXIT & 1) && (FEAT & F_SMALL) != 0u && !INL &&
+                 (FEAT & (F_CORNELL | F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) == 0u) ||
+                ((VR_WAVE_AT_EXIT & 2) && CORN && !INL && (FEAT & F_SMALL) == 0u) ||
+                ((VR_WAVE_AT_EXIT & 4) && CORN && INL);
             if constexpr (AT_EXIT) {
-                if (bounce_step<CNT, FEAT, false>(p, ray, hr, ps, out, cnt, [&](const vr4& o) {
-                        store_path_rgb(p, q, slot, o);
-                        if (p.path_cost)
-                            p.path_cost[(size_t)q * p.path_stride + slot] = (uint8_t)(cnt.work < 510u ? cnt.work >> 1 : 255u);
+                if (bounce_step<CNT, FEAT, INL && !EARLY_DEPTH>(p, ray, hr, ps, out, cnt, [&](const vr4& o) {
+                        if constexpr (INL && !EARLY_DEPTH) store_path(p, lane_q(), lane_slot(), o, ps.depth);
+                        else store_path_rgb(p, lane_q(), lane_slot(), o);
+                        if constexpr ((FEAT & F_SMALL) != 0u) {
+                            if (p.path_cost)
+                                p.path_cost[(size_t)lane_q() * p.path_stride + lane_slot()] =
+                                    (uint8_t)(cnt.work < 510u ? cnt.work >> 1 : 255u);
+                        }
                     })) {
                     ended = true;
                 } else {
