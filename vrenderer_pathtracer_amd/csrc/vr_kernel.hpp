@@ -1702,10 +1702,17 @@ __device__ __forceinline__ uint32_t queue_item(uint32_t q, uint32_t v, uint32_t 
 #endif
 }
 
+// The textured small-launch kernels (C3 shards) keep a path's index in LDS,
+// 4 B per lane taken from the node cache (wave_body lane_q)
+template <uint32_t FEAT>
+constexpr bool lds_q() {
+    return (FEAT & F_SMALL) != 0u && (FEAT & (F_INLINE_PRIM | F_SERVICE)) == 0u &&
+           (FEAT & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
+}
 template <int STACK, uint32_t FEAT, int BT>
 __global__ void __launch_bounds__(BT, path_waves(STACK, cornell_kernel<FEAT>())) render_wave_kernel(const RenderParams p)
 {
-    constexpr int CN = path_cache_nodes(STACK, BT, cornell_kernel<FEAT>());
+    constexpr int CN = path_cache_nodes(STACK, BT, cornell_kernel<FEAT>()) - (lds_q<FEAT>() ? (4 * BT + 55) / 56 : 0);
     __shared__ int lds_stack[STACK * BT];
     __shared__ vr4 lds_nodes[3 * CN];
     __shared__ int2 lds_idx[CN];
@@ -1819,7 +1826,10 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     // only moved theirs).  While a lane helps (help_step), `slot` holds its
     // owner's lane as everywhere.
     constexpr bool PACKQ = (FEAT & F_INLINE_PRIM) != 0u && (FEAT & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
-    auto lane_q = [&]() -> uint32_t { return PACKQ ? (slot & 1u) : q; };
+    // the textured small-launch kernels keep it in LDS (lds_q: 3 spills -> 0)
+    constexpr bool LDSQ = lds_q<FEAT>();
+    __shared__ uint32_t lds_path[LDSQ ? BT : 1];
+    auto lane_q = [&]() -> uint32_t { return PACKQ ? (slot & 1u) : LDSQ ? lds_path[tid] : q; };
     auto lane_slot = [&]() -> uint32_t { return PACKQ ? (slot >> 1) : slot; };
     uint32_t cam_xy = 0;                                   // F_INLINE_PRIM: its pixel (x << 16 | y) until LS_CAMERA
     Ray ray;
@@ -1832,6 +1842,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
     auto start = [&](uint32_t sub, uint32_t path, uint32_t px) {   // render's per-sample prologue (:817-844)
         if (sub == ~0u) { state = LS_DONE; return; }
         q = path;
+        if constexpr (LDSQ) lds_path[tid] = path;
         slot = sub * 64u + px;
         if constexpr (SPARSE) {                            // the listed pixel
             const uint32_t k = slot < n_px ? slot : n_px - 1u;
