@@ -725,3 +725,36 @@ def test_hdr_storage_bitexact_vs_portable_oracle(native, oracle, halves):
     ga, grgba, _, _ = gpu_render(sc, 2, times)
     assert_bitexact(ga, oa, sc, "accum")
     assert_bitexact(grgba, orgba, sc, "rgba8")
+
+
+def test_kernel_timing_switch(native):
+    """vrhip_set_kernel_timing(0) (the Qt adapter's setting): no kernel-span
+    events on the launch path -- kernel_stats counts no launch and
+    last_kernel_ms reads 0 -- and the images are those of the default; back
+    on, the next launch is timed again."""
+    sc = scenes.make_scene("C2", 96, 64)
+    times = [sc["time"] + i for i in range(3)]
+
+    def run(timing):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_kernel_timing(timing)
+        r.kernel_stats(reset=True)
+        for t in times:
+            r.render(frames=1, times=[t])
+        ms, n = r.kernel_stats()
+        last = r.last_kernel_ms()
+        out = r.read_accum(), r.read_rgba8()
+        if not timing:
+            r.set_kernel_timing(True)
+            r.render(frames=1, times=[times[-1] + 1])
+            ms2, n2 = r.kernel_stats()
+            assert n2 == 1 and ms2 > 0 and r.last_kernel_ms() > 0
+        r.cleanUp()
+        return out, n, last
+
+    (a0, c0), n0, last0 = run(False)
+    (a1, c1), n1, last1 = run(True)
+    assert n0 == 0 and last0 == 0.0
+    assert n1 == 3 and last1 > 0
+    assert np.array_equal(a0.view(np.uint32), a1.view(np.uint32)) and np.array_equal(c0, c1)
