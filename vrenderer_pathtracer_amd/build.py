@@ -85,7 +85,7 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None, out_path
                 print(res.stderr, file=sys.stderr)
             if res.returncode != 0:
                 raise RuntimeError(f"hipcc failed on {src}:\n" + res.stdout + res.stderr)
-        tmp = out + ".tmp"
+        tmp = f"{out}.tmp{os.getpid()}"      # ranks that build at once each link their own file
         cmd = [hipcc] + HIPCC_FLAGS + list(extra_flags or []) + ["-o", tmp] + objs + ["-lz", "-lrccl"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
