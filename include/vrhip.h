@@ -379,6 +379,12 @@ int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t 
 /* The same for the kernels' square root (sqrt_rn: v_sqrt_f32 + the neighbour
  * tests of the IEEE expansion) against sqrtf, positive patterns only. */
 int vrhip_selftest_sqrt(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t *mismatches, uint32_t *first_bad);
+/* Exhaustive check of the table tonemap (no reference counterpart): the
+ * colour byte the kernels take from the context's threshold table against
+ * the byte of f2u8(pow(c, 1/2.2) * 255) (PathTracer.cu:850-866, the f64
+ * pow), for every float bit pattern c in [lo_bits, hi_bits) (and -0.0 when
+ * lo_bits is 0); the range [0, 0x3f800001) is every clamped channel value. */
+int vrhip_selftest_tonemap(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t *mismatches, uint32_t *first_bad);
 
 /* ---- host-side helpers (no device needed) ----------------------------- */
 /* Native BVH build + reference flattening (src/vRendererCuda.cpp:204-279)

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import pyoracle as po
-from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math, selftest_rcp, selftest_sqrt
+from vrenderer_pathtracer_amd import VRendererHIP, scenes, selftest_math, selftest_rcp, selftest_sqrt, selftest_tonemap
 from vrenderer_pathtracer_amd._native import VRHIPError
 
 pytestmark = pytest.mark.gpu
@@ -109,6 +109,15 @@ def test_rcp_exhaustive(native):
     hi = int(np.float32(2.0 ** 125).view(np.uint32)) + 1
     n, first = selftest_rcp(lo, hi)
     assert n == 0, f"{n} mismatches, first {first:#010x}"
+
+
+def test_tonemap_table_exhaustive(native):
+    """The table tonemap (vr_kernel.hpp tone_byte: the hardware log2 / exp2
+    estimate checked against the context's 256 thresholds) gives the byte of
+    f2u8(pow(c, 1/2.2) * 255) with the f64 pow for every float c in [-0, 1]
+    -- every value a clamped channel can take."""
+    n, first = selftest_tonemap(0, 0x3F800001)
+    assert n == 0, (n, hex(first))
 
 
 def test_sqrt_exhaustive(native):

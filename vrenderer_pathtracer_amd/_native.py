@@ -99,6 +99,8 @@ _SIGNATURES = {
     "vrhip_selftest_math": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _f, _f, _f, ctypes.c_size_t]),
     "vrhip_selftest_rcp": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.POINTER(ctypes.c_uint64), _u32]),
+    "vrhip_selftest_tonemap": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.POINTER(ctypes.c_uint64), _u32]),
     "vrhip_selftest_sqrt": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.POINTER(ctypes.c_uint64), _u32]),
     "vrhip_build_flat": (ctypes.c_int, [_f, _f, _f, _f, ctypes.c_uint32, _u32, ctypes.c_uint32, ctypes.c_uint32,

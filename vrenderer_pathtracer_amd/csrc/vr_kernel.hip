@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     const unsigned char db = f2u8((1.f - last_w) * 255);
     u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
     p.depth[ind] = dv;
-    p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
+    p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u, p.tone_t);
     p.accum[ind] = io;
     if (p.path_cost) {
         // the sub-tile's cost for the next launch's order: its paths' costs,
@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(kBlockThreads) svc_finish_kernel(const RenderP
         frame += f.n_frames[L];
         if (f.gather[L]) {
             uint8_t* st = f.staging + (size_t)L * f.stage_bytes;
-            if (f.gather[L] & 1u) reinterpret_cast<u8x4*>(st)[packed] = tonemap(io, frame - 1u);
+            if (f.gather[L] & 1u) reinterpret_cast<u8x4*>(st)[packed] = tonemap(io, frame - 1u, p.tone_t);
             if (f.gather[L] & 4u) {
                 const unsigned char db = f2u8((1.f - last_w) * 255);
                 u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(kBlockThreads) svc_finish_kernel(const RenderP
     const unsigned char db = f2u8((1.f - last_w) * 255);
     u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
     p.depth[ind] = dv;
-    p.rgba[ind] = tonemap(io, frame - 1u);
+    p.rgba[ind] = tonemap(io, frame - 1u, p.tone_t);
     p.accum[ind] = io;
 }
 
@@ -310,18 +310,27 @@ int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t 
 // float bit patterns [lo, hi): fn 0 rcp_rn vs 1.f / x (both signs), fn 1
 // sqrt_rn vs sqrtf (positive x).  Counts mismatches, records the smallest
 // mismatching pattern.
-__global__ void selftest_exact_kernel(int fn, uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad)
+// fn 2: the table tonemap byte (tone_byte) vs the f64 one (tone_byte_ref)
+// over [lo, hi) and -0.0
+__global__ void selftest_exact_kernel(int fn, uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad,
+                                      const float* T)
 {
     const uint32_t stride = gridDim.x * blockDim.x;        // hi <= 2^31: b + stride cannot wrap
     unsigned long long bad = 0;
     uint32_t first = 0xffffffffu;
     for (uint32_t b = lo + blockIdx.x * blockDim.x + threadIdx.x; b < hi; b += stride) {
-        for (int neg = 0; neg < (fn == 0 ? 2 : 1); ++neg) {
+        for (int neg = 0; neg < (fn == 0 || (fn == 2 && b == 0u) ? 2 : 1); ++neg) {
             const uint32_t bits = neg ? (b | 0x80000000u) : b;
             const float x = __uint_as_float(bits);
-            const float got = fn == 0 ? rcp_rn(x) : sqrt_rn(x);
-            const float want = fn == 0 ? 1.f / x : __builtin_sqrtf(x);
-            if (__float_as_uint(got) != __float_as_uint(want)) {
+            bool diff;
+            if (fn == 2) {
+                diff = tone_byte(x, T) != tone_byte_ref(x);
+            } else {
+                const float got = fn == 0 ? rcp_rn(x) : sqrt_rn(x);
+                const float want = fn == 0 ? 1.f / x : __builtin_sqrtf(x);
+                diff = __float_as_uint(got) != __float_as_uint(want);
+            }
+            if (diff) {
                 ++bad;
                 first = bits < first ? bits : first;
             }
@@ -334,10 +343,32 @@ __global__ void selftest_exact_kernel(int fn, uint32_t lo, uint32_t hi, unsigned
 }
 
 int launch_selftest_exact(int fn, uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad,
-                          void* stream)
+                          const float* tone_t, void* stream)
 {
     hipLaunchKernelGGL(selftest_exact_kernel, dim3(4096), dim3(256), 0, (hipStream_t)stream, fn, lo, hi, n_bad,
-                       first_bad);
+                       first_bad, tone_t);
+    return (int)hipGetLastError();
+}
+
+// The tonemap threshold table (tone_byte): T[k] = the smallest float c in
+// [0, 1] whose byte tone_byte_ref(c) >= k, by bisection over the bit
+// patterns (tone_byte_ref(1) = 255); T[0] = 0.
+__global__ void tone_table_kernel(float* T)
+{
+    const uint32_t k = threadIdx.x;
+    if (k == 0) { T[0] = 0.f; return; }
+    uint32_t lo = 0u, hi = 0x3f800000u;
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (tone_byte_ref(__uint_as_float(mid)) >= k) hi = mid;
+        else lo = mid + 1u;
+    }
+    T[k] = __uint_as_float(lo);
+}
+
+int launch_tone_table(float* T, void* stream)
+{
+    hipLaunchKernelGGL(tone_table_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, T);
     return (int)hipGetLastError();
 }
 

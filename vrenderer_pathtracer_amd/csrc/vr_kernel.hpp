@@ -1107,15 +1107,40 @@ __device__ __forceinline__ vr4 trace(const RenderParams& p, Ray ray, const HitRe
     }
 }
 
+// One colour byte of the tonemap (PathTracer.cu:850-866): f2u8 of
+// pow(c, 1/2.2) * 255 for the clamped channel c in [0, 1] (clampf maps NaN
+// to 1 and leaves -0.0, whose byte is 0).
+__device__ __forceinline__ unsigned char tone_byte_ref(float c) { return f2u8(pow_p(c, 1.f / 2.2f) * 255); }
+// The same byte from the context's threshold table (RenderParams::tone_t,
+// tone_table_kernel): T[k] = the smallest c with tone_byte_ref(c) >= k, so
+// the byte is the number of thresholds in (0, c] -- found from the hardware
+// log2 / exp2 estimate (off by at most one) and checked against T[k] and
+// T[k + 1].  Equal to tone_byte_ref for every float in [-0, 1]: an
+// exhaustive comparison (vrhip_selftest_tonemap) shows the byte is
+// monotonic there.  Two table loads instead of the f64 log2 / exp2 of
+// pow_p: the one-frame finish pass 23.4 -> 16.9 us on C2 (r05w).
+__device__ __forceinline__ unsigned char tone_byte(float c, const float* __restrict__ T)
+{
+    int k = (int)(__builtin_amdgcn_exp2f(__builtin_amdgcn_logf(c) * (1.f / 2.2f)) * 255.f);
+    k = k < 0 ? 0 : (k > 255 ? 255 : k);
+    while (k < 255 && c >= T[k + 1]) ++k;
+    while (k > 0 && c < T[k]) --k;
+    return (unsigned char)k;
+}
 // colour of the accumulated radiance after `frame` frames (PathTracer.cu:850-866)
-__device__ __forceinline__ u8x4 tonemap(vr4 io, uint32_t frame) {
+__device__ __forceinline__ u8x4 tonemap(vr4 io, uint32_t frame, const float* __restrict__ T) {
     const float coef = 1.f / (float)frame;
     const vr4 sc = mul4s(io, coef);
-    const float inv_gamma = 1.f / 2.2f;
     u8x4 c;
-    c.x = f2u8(pow_p(clampf(sc.x, 0.f, 1.f), inv_gamma) * 255);
-    c.y = f2u8(pow_p(clampf(sc.y, 0.f, 1.f), inv_gamma) * 255);
-    c.z = f2u8(pow_p(clampf(sc.z, 0.f, 1.f), inv_gamma) * 255);
+    if (T) {
+        c.x = tone_byte(clampf(sc.x, 0.f, 1.f), T);
+        c.y = tone_byte(clampf(sc.y, 0.f, 1.f), T);
+        c.z = tone_byte(clampf(sc.z, 0.f, 1.f), T);
+    } else {
+        c.x = tone_byte_ref(clampf(sc.x, 0.f, 1.f));
+        c.y = tone_byte_ref(clampf(sc.y, 0.f, 1.f));
+        c.z = tone_byte_ref(clampf(sc.z, 0.f, 1.f));
+    }
     c.w = 0xff;
     return c;
 }
@@ -1303,7 +1328,7 @@ __global__ void __launch_bounds__(kBlockThreads, render_waves<FEAT>(STACK)) rend
         const unsigned char db = f2u8((1.f - last_w) * 255);
         u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
         p.depth[ind] = dv;
-        p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u);
+        p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u, p.tone_t);
         p.accum[ind] = io;
     }
     if (COUNT) flush_counts(p, cnt, lane, (FEAT & F_COUNT_EXEC) != 0u);

@@ -166,6 +166,7 @@ struct RenderParams {
     uint32_t small_blocks;           // render_wave_kernel: 256-thread blocks (launches of < 2^24 paths)
     uint32_t n_queues;               // render_wave_kernel: work queue heads in use (VR_QUEUES / VR_QUEUES_LARGE)
     uint32_t inline_prim;            // paths trace their own camera ray (no primary_kernel pass; F_INLINE_PRIM kernel)
+    const float* tone_t;             // the tonemap threshold table (vr_kernel.hpp tone_byte; nullptr: f64 pow)
     const vr4* bvh;
     const vr4* bvh16;                // same nodes, conservative fp16 boxes, 32 B each (culled traversal)
     uint32_t n_nodes;                // inner nodes in bvh (4 rows each, area-ordered)
@@ -222,6 +223,8 @@ int launch_vmem_roof(int width, const uint32_t* tab, uint32_t n_lines, uint32_t 
                      uint32_t blocks, uint32_t* out, void* stream);
 int launch_selftest_math(int fn, const float* a, const float* b, float* out, size_t n, void* stream);
 int launch_selftest_exact(int fn, uint32_t lo, uint32_t hi, unsigned long long* n_bad, uint32_t* first_bad,
-                          void* stream);
+                          const float* tone_t, void* stream);
+// the tonemap threshold table (256 floats; vr_kernel.hpp tone_byte)
+int launch_tone_table(float* T, void* stream);
 
 } // namespace vr

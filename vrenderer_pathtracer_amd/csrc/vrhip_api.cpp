@@ -147,6 +147,7 @@ struct vrhip_ctx {
     // every launch's render kernels (vrhip_kernel_stats) and each call
     // (vrhip_last_kernel_ms)
     bool kernel_timing = true;
+    float* tone_t = nullptr;     // the tonemap threshold table (vr_kernel.hpp tone_byte), filled at creation
     double kernel_ms_total = 0.0;    // union of the launches' render-kernel spans (overlapping launches count once)
     uint64_t launches_total = 0;
     uint32_t last_split = 1, last_use_scratch = 0, last_kind = 0;   // vrhip_last_launch_info
@@ -572,6 +573,9 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     }
     if (hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
         return cleanup(fail(VRHIP_ERR_HIP, "hipEventCreate failed"));
+    if (hipMalloc((void**)&c->tone_t, 256 * sizeof(float)) != hipSuccess ||
+        vr::launch_tone_table(c->tone_t, c->stream) != 0)
+        return cleanup(fail(VRHIP_ERR_HIP, "tonemap table setup failed"));
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         c->cu_count = (uint32_t)cus;
@@ -621,7 +625,7 @@ int vrhip_destroy(vrhip_ctx* c)
     dfree(c->hdr); dfree(c->tex[0]); dfree(c->tex[1]); dfree(c->tex[2]); dfree(c->brdf);
     for (int i = 0; i < 2; ++i)
         if (c->gl_res[i]) (void)hipGraphicsUnregisterResource(c->gl_res[i]);
-    dfree(c->counters);
+    dfree(c->counters); dfree(c->tone_t);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     dfree(c->comm_send); dfree(c->comm_recv);
     for (auto& l : c->lane) {
@@ -1323,6 +1327,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     p.cy = vr4{ c->fov_scale * c->cam_up[0], c->fov_scale * c->cam_up[1], c->fov_scale * c->cam_up[2], 0.f };
     p.W = c->W; p.H = c->H;
     p.cam_sxy = c->cam_sxy;
+    p.tone_t = c->tone_t;
     p.wr = (c->W / 16u) * 16u; p.hr = rendered_rows(c);
     p.fresnel_coef = c->fresnel_coef; p.fresnel_pow = c->fresnel_pow;
     uint32_t f = 0;
@@ -2025,12 +2030,18 @@ static int selftest_exact(int fn, int device, uint32_t lo_bits, uint32_t hi_bits
     const uint32_t init_first = 0xffffffffu;
     HIP_TRY(hipMemset(d, 0, 8));
     HIP_TRY(hipMemcpy(df, &init_first, 4, hipMemcpyHostToDevice));
-    int e = vr::launch_selftest_exact(fn, lo_bits, hi_bits, d, df, nullptr);
-    if (e) { (void)hipFree(d); return fail(VRHIP_ERR_HIP, "selftest launch failed"); }
+    float* T = nullptr;
+    if (fn == 2) {                                        // the tonemap table under test
+        HIP_TRY(hipMalloc((void**)&T, 256 * sizeof(float)));
+        if (vr::launch_tone_table(T, nullptr)) { (void)hipFree(d); (void)hipFree(T); return fail(VRHIP_ERR_HIP, "tone table launch failed"); }
+    }
+    int e = vr::launch_selftest_exact(fn, lo_bits, hi_bits, d, df, T, nullptr);
+    if (e) { (void)hipFree(d); if (T) (void)hipFree(T); return fail(VRHIP_ERR_HIP, "selftest launch failed"); }
     unsigned long long n = 0;
     HIP_TRY(hipMemcpy(&n, d, 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost));
     (void)hipFree(d);
+    if (T) (void)hipFree(T);
     *mismatches = n;
     return VRHIP_OK;
 }
@@ -2043,6 +2054,11 @@ int vrhip_selftest_rcp(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t*
 int vrhip_selftest_sqrt(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches, uint32_t* first_bad)
 {
     return selftest_exact(1, device, lo_bits, hi_bits, mismatches, first_bad);
+}
+
+int vrhip_selftest_tonemap(int device, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches, uint32_t* first_bad)
+{
+    return selftest_exact(2, device, lo_bits, hi_bits, mismatches, first_bad);
 }
 
 int vrhip_build_flat(const float* positions, const float* normals, const float* tangents, const float* uvs,

@@ -504,6 +504,17 @@ def selftest_rcp(lo_bits: int, hi_bits: int, device: int = 0):
     return int(n.value), int(first.value)
 
 
+def selftest_tonemap(lo_bits: int = 0, hi_bits: int = 0x3F800001, device: int = 0):
+    """Exhaustively compare the kernels' table tonemap byte with the f64
+    pow byte over the float bit patterns [lo_bits, hi_bits) (+ -0.0):
+    (mismatches, first_bad)."""
+    n = ctypes.c_uint64(0)
+    first = ctypes.c_uint32(0)
+    check(_native.lib().vrhip_selftest_tonemap(device, lo_bits, hi_bits, ctypes.byref(n), ctypes.byref(first)),
+          "vrhip_selftest_tonemap")
+    return int(n.value), int(first.value)
+
+
 def selftest_sqrt(lo_bits: int, hi_bits: int, device: int = 0):
     """Exhaustively compare the kernels' square root with sqrtf over the float
     bit patterns [lo_bits, hi_bits): (mismatches, first_bad)."""
