@@ -500,8 +500,11 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 #ifndef VR_NODE_BREAK_CORNELL
 // Cornell-box kernels (every bounce ray stays inside the box and most lanes
 // keep traversing the mesh): r02 6-wave kernel, C2 6: 3,910, 10: 3,986;
-// the HDRI scenes lose at 10 (C3 -1.3 %, C5 -1.2 %) and keep VR_NODE_BREAK
-#define VR_NODE_BREAK_CORNELL 10
+// the HDRI scenes lose at 10 (C3 -1.3 %, C5 -1.2 %) and keep VR_NODE_BREAK.
+// Re-measured on the r05 7-wave service kernel (profiles/r05x_node_break_*):
+// C2 8: -1.2 %, 12: +1.0 %, 14: +1.9 %, 16: +2.0-2.4 %, 20: +1.7-2.0 %
+// against 10 (C2D 16: +1.2-2.2 %)
+#define VR_NODE_BREAK_CORNELL 16
 #endif
 // Kernels over the listed pixels of HDRI scenes (F_SPARSE: every lane's path
 // hit the mesh at its camera ray): 8 (r04, against 6: C3 +0.7 %, C5 +0.7 %,
