@@ -494,8 +494,14 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 // leaf postponed (:345-351), then the leaf loop.  tr.nodeAddr is an inner
 // node, a leaf (a helper's first entry) or kSentinel (no-op).
 #ifndef VR_NODE_BREAK
-#define VR_NODE_BREAK 6    // measured (path kernel with paired triangle loads): 0 (the reference's
-                           // all-lanes vote) C2 2,294, 2: 2,503, 4: 2,563, 6: 2,577, 8: 2,583 (C3 -2 %)
+// measured (path kernel with paired triangle loads): 0 (the reference's
+// all-lanes vote) C2 2,294, 2: 2,503, 4: 2,563, 6: 2,577, 8: 2,583 (C3 -2 %).
+// Since the Cornell-box and listed-pixel kernels have their own thresholds
+// (below) this one serves the one-frame kernels and the HDRI primary-pass
+// kernels: r05, 8 against 6, one frame per call C2 0.695 -> 0.686 ms, C3
+// 0.398 -> 0.393, C5 1.717 -> 1.707 (4: +1.5-2 % slower), 16-frame rates
+// unchanged (profiles/r05x_node_break_one_frame_*.txt)
+#define VR_NODE_BREAK 8
 #endif
 #ifndef VR_NODE_BREAK_CORNELL
 // Cornell-box kernels (every bounce ray stays inside the box and most lanes
@@ -515,8 +521,8 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 template <uint32_t FEAT>
 constexpr int node_break() {
     if ((FEAT & F_SPARSE) != 0u) return VR_NODE_BREAK_SPARSE;
-    // one-frame kernels (F_INLINE_PRIM) keep 6: the interactive C2 rate fell
-    // 2,147 -> 2,103 Mpaths/s with 10 (r02h)
+    // one-frame kernels (F_INLINE_PRIM) keep VR_NODE_BREAK: the interactive
+    // C2 rate fell 2,147 -> 2,103 Mpaths/s with 10 (r02h)
     return ((FEAT & (F_EXACT | F_CLASS)) && (FEAT & F_CORNELL) && !(FEAT & F_INLINE_PRIM)) ? VR_NODE_BREAK_CORNELL : VR_NODE_BREAK;
 }
 // The node-loop exit is proportional to the lanes in the call: a full wave
