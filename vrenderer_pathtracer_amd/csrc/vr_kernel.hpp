@@ -501,7 +501,8 @@ __device__ __forceinline__ void tri_test_v(const RenderParams& p, const Ray& r, 
 // kernels: r05, 8 against 6, one frame per call C2 0.695 -> 0.686 ms, C3
 // 0.398 -> 0.393, C5 1.717 -> 1.707 (4: +1.5-2 % slower), 16-frame rates
 // unchanged (profiles/r05x_node_break_one_frame_*.txt); 12 against 8: C2
-// 0.687 -> 0.677, C3 0.394 -> 0.389 (profiles/r05y_node_break12_one_frame_*)
+// 0.687 -> 0.677, C3 0.394 -> 0.389 (profiles/r05y_node_break12_one_frame_*);
+// 16 ties, 20 loses (profiles/r05z_node_break16_20_one_frame_*)
 #define VR_NODE_BREAK 12
 #endif
 #ifndef VR_NODE_BREAK_CORNELL
