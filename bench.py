@@ -41,6 +41,11 @@ from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes in profiles/).  The reference
 algorithm's bytes (SURVEY.md 8d pricing) are reported separately.
 cpu_baseline = the CPU oracle (oracle/, a C restatement of the reference
 kernel) on a bounded sample of the same workload on this host's cores.
+verified = after the timed loop its first steps are rendered again through
+the render service and launch by launch; the SHA-256 digests of the two
+accumulations (and RGBA8 images) must agree on every rank, else the bench
+exits with status 3.  build = the library's embedded source hash
+(vrhip_build_id) and whether it matches the sources on disk.
 """
 from __future__ import annotations
 
@@ -204,6 +209,48 @@ def cpu_baseline(scene: dict, budget_s: float) -> dict:
     return out
 
 
+# ---- self-check of the timed image ---------------------------------------------
+VERIFY_STEPS = 3
+
+
+def self_check(r, scene: dict, F: int, svc_mode: int, world: int, red_dev) -> dict:
+    """Render the timed loop's first VERIFY_STEPS steps (same frame counts and
+    times) twice from a cleared accumulation: through the render service
+    (vrhip_set_service(1): every launch on the session kernel the timed steps
+    run on, the sessions' multi-slot finish pass) and launch by launch
+    (vrhip_set_service(0)); SHA-256 of each run's accumulation (float4 bits)
+    and RGBA8 image.  verified = the digests agree on every rank.  The
+    renderer is left cleared, in service mode svc_mode."""
+    import hashlib
+    import torch
+    import torch.distributed as dist
+    runs = {}
+    for label, mode in (("service", 1), ("launch_path", 0)):
+        r.set_service(mode)
+        r.clearBuffer()
+        kinds = []
+        for i in range(VERIFY_STEPS):
+            r.render(frames=F, times=[scene["time"] + i * F + k for k in range(F)], sync=False)
+            kinds.append(r.last_launch_info()["kind"])
+        r.sync()
+        acc, rgba = r.read_accum(), r.read_rgba8()
+        runs[label] = {"accum_sha256": hashlib.sha256(acc.tobytes()).hexdigest(),
+                       "rgba8_sha256": hashlib.sha256(rgba.tobytes()).hexdigest(), "kinds": kinds}
+    r.set_service(svc_mode)
+    r.clearBuffer()
+    r.sync()
+    same = int(runs["service"]["accum_sha256"] == runs["launch_path"]["accum_sha256"]
+               and runs["service"]["rgba8_sha256"] == runs["launch_path"]["rgba8_sha256"])
+    ok = torch.tensor([float(same)], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return {"verified": bool(ok.item() == 1.0), "steps": VERIFY_STEPS, "frames_per_step": F,
+            "service": runs["service"], "launch_path": runs["launch_path"],
+            "note": "the timed loop's first steps re-rendered from a cleared accumulation through the render service "
+                    "(mode 1) and launch by launch (mode 0); SHA-256 of accum and RGBA8 (this rank's; all ranks "
+                    "agree when verified)"}
+
+
 # ---- main ---------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -269,7 +316,7 @@ def main():
             raise SystemExit(f"bench.py: process group formed {formed} ranks, --gpus {args.gpus}")
     red_dev = dev if backend == "nccl" else torch.device("cpu")
 
-    from vrenderer_pathtracer_amd import VRendererHIP, build_native, scenes
+    from vrenderer_pathtracer_amd import VRendererHIP, build_id, build_native, scenes
     from vrenderer_pathtracer_amd.tiles import TileGather, WHAT_RGBA8
     build_native()
     CFG = args.config
@@ -284,6 +331,14 @@ def main():
     owned = r.owned_pixels()
     gather = TileGather(r, rank, world, dev, WHAT_RGBA8)
     mesh = scene.get("mesh_flat") is not None
+    # N > 1: explicit render-service mode, so a step's RCCL gather is deferred
+    # to the session's close and consecutive steps share one session (their
+    # drains overlap); every rank closes its session (r.sync()) before any
+    # host barrier, the ordering include/vrhip.h asks of explicit mode.  One
+    # rank: the library default (automatic: the first call of a burst on the
+    # launch path, the calls behind it on the service)
+    svc_mode = 1 if (world > 1 and gather.native) else -1
+    r.set_service(svc_mode)
 
     # untimed counting steps on this rank's share: (1) the reference
     # algorithm's events (strict traversal, no primary-hit reuse, no last-
@@ -331,6 +386,17 @@ def main():
 
     wr = (W // 16) * 16
     hr = (H // 16) * 16
+
+    # self-check of the timed path: the first VERIFY_STEPS steps of the timed
+    # loop rendered again from a cleared accumulation, once on the render
+    # service (mode 1: every launch through the session kernel the timed
+    # steps ran on) and once launch by launch (mode 0), with the same times;
+    # SHA-256 of the accumulation and RGBA8 image must agree on every rank
+    verify = self_check(r, scene, F, svc_mode, world, red_dev)
+    if rank == 0 and not verify["verified"]:
+        print(json.dumps({"metric": METRIC, "verified": False, "verify": verify}), flush=True)
+    if not verify["verified"]:
+        raise SystemExit(3)
 
     def timed_steps(rr, frames, steps, base, with_gather=True):
         """max-over-ranks wall time of `steps` back-to-back steps of `frames`
@@ -408,8 +474,10 @@ def main():
     if args.interactive_frames > 0:
         r.clearBuffer()
         # the Qt adapter's configuration (integration/vRendererHIP.cpp): no
-        # kernel-timing events on the launch path (nothing reads them there)
+        # kernel-timing events on the launch path (nothing reads them there),
+        # the library's automatic service mode
         r.set_kernel_timing(False)
+        r.set_service(-1)
         base = scene["time"] + 100000
         for i in range(3):
             r.render(frames=1, times=[base + i], sync=True)
@@ -581,6 +649,9 @@ def main():
             "samples_weak": samples_weak,
             "interactive": inter,
             "roofline": roofline,
+            "verified": verify["verified"],
+            "verify": verify,
+            "build": build_id(),
         }
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(scene, args.cpu_budget)

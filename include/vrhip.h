@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define VRHIP_ABI_VERSION 3
+#define VRHIP_ABI_VERSION 4
 
 typedef enum vrhip_status {
     VRHIP_OK = 0,
@@ -41,6 +41,10 @@ typedef struct vrhip_ctx vrhip_ctx;
 /* Thread-local text of the last error. */
 const char *vrhip_last_error(void);
 int vrhip_abi_version(void);
+/* SHA-256 (hex) of the sources, this header and the compile flags the
+ * library was built from; the Python loader rebuilds when it differs from
+ * the files on disk, and bench.py / smoke() print it. */
+const char *vrhip_build_id(void);
 int vrhip_device_count(int *count);
 
 /* ---- lifetime -------------------------------------------------------- */
@@ -242,14 +246,34 @@ int vrhip_set_overlap(vrhip_ctx *ctx, int mode);
  * -- unsynchronised back-to-back calls, not the first call of a burst; also
  * whole frames of HDRI mesh scenes behind a launch in flight.  Launches whose
  * result slots the service's scratch budget (VRHIP_SERVICE_BYTES, default 24
- * GiB) cannot hold twice take the ordinary launch path in every mode.  The
+ * GiB; a session's slots also take at most half of the device memory free when
+ * it opens) cannot hold twice take the ordinary launch path in every mode, as
+ * do the launches of a session whose scratch allocation fails.  The
  * open session's kernel retires after 20 ms without a new launch; a launch
  * posted while it retires is detected (a store-fence-load hand-shake on the
- * ring) and rendered through the launch path instead.  Deferred gathers:
- * the ncclGather of a vrhip_comm_gather inside a session is enqueued when the
- * session closes -- at the latest by the next vrhip call on the context that is
- * not vrhip_render or vrhip_comm_gather, so a rank must call vrhip_sync (or any
- * read-back) before it blocks in a host-side barrier with the other ranks. */
+ * ring) and rendered through the launch path instead.
+ * Gathers (vrhip_comm_gather) inside a session:
+ *   mode -1 (automatic): the gather closes the session and is enqueued at
+ *   once, like outside a session -- no collective ever waits on a later host
+ *   call, whatever the caller does next.
+ *   mode 1 (explicit): the gather is DEFERRED -- the image as of that call is
+ *   staged by the session's finish pass and its ncclGather enqueued when the
+ *   session closes, so consecutive steps keep one session (their drains
+ *   overlap).  The caller then owns the ordering: a rank must close its
+ *   session before it blocks on anything the other ranks' gathers wait for
+ *   (a host barrier, a device-wide synchronise).  Calls that close a session:
+ *   vrhip_sync, vrhip_read_accum/rgba8/depth8, vrhip_device_buffers,
+ *   vrhip_gl_present, vrhip_pack_tiles/unpack_tiles, vrhip_last_kernel_ms,
+ *   vrhip_kernel_stats, vrhip_debug_counters, vrhip_set_camera, vrhip_clear,
+ *   every upload, vrhip_set_stream, vrhip_set_tiling, vrhip_set_service
+ *   (and its timing / budget hooks), vrhip_comm_init/destroy, vrhip_destroy,
+ *   the counting renders, and a vrhip_render that does not fit the session.
+ *   Calls that do NOT close it: the flag setters (Cornell box, example sphere,
+ *   BRDF, strict traversal, Fresnel -- the next vrhip_render then no longer
+ *   fits and closes it), vrhip_set_overlap, vrhip_set_path_split,
+ *   vrhip_set_kernel_timing, and the queries vrhip_frame_count,
+ *   vrhip_last_launch_info, vrhip_owned_pixels, vrhip_service_stats/info,
+ *   vrhip_device_group, vrhip_bvh_info, vrhip_get_stream. */
 int vrhip_set_service(vrhip_ctx *ctx, int mode);
 /* Render-service timing (test hook, no reference counterpart; 0 = default):
  * the session kernel's idle limit (20 ms), the host's window for posting to
@@ -265,6 +289,14 @@ int vrhip_set_service_budget(vrhip_ctx *ctx, size_t bytes);
 /* Launches that met a retiring session kernel and took the launch path
  * instead (since the context was created). */
 int vrhip_service_stats(vrhip_ctx *ctx, uint64_t *refused_launches);
+/* Render-service counts since the context was created (diagnostics; no
+ * reference counterpart): out[0] launches refused by a retiring kernel (as
+ * vrhip_service_stats), [1] sessions opened, [2] launches sessions took,
+ * [3] gathers deferred to a session's close (explicit mode 1 only), [4]
+ * sessions not opened because their scratch could not be allocated (those
+ * launches took the launch path). */
+#define VRHIP_SERVICE_INFO 5
+int vrhip_service_info(vrhip_ctx *ctx, uint64_t out[VRHIP_SERVICE_INFO]);
 /* Frames rendered since the last clear (vRendererCuda::getFrameCount,
  * include/vRendererCuda.h:124). */
 int vrhip_frame_count(vrhip_ctx *ctx, uint32_t *frames);
@@ -319,9 +351,10 @@ int vrhip_comm_init(vrhip_ctx *ctx, uint32_t rank, uint32_t n_ranks, const uint8
  * 2 depth8), ONE ncclGather brings them to rank 0, and rank 0 scatters them
  * into its full image -- all enqueued on the context stream behind the
  * render's finish passes (no host synchronisation).  Rank 0's image `what`
- * then holds the whole frame.  Inside a render-service session the gather is
- * deferred to the session's close (vrhip_set_service): call vrhip_sync before
- * any host-side barrier between ranks. */
+ * then holds the whole frame.  Inside a render-service session it closes the
+ * session first (automatic service mode, the default), or, in explicit
+ * service mode 1, is deferred to the session's close -- then call vrhip_sync
+ * before any host-side barrier between ranks (vrhip_set_service). */
 int vrhip_comm_gather(vrhip_ctx *ctx, int what);
 /* Leaves the communicator (waits for the context stream first).  vrhip_destroy does it too. */
 int vrhip_comm_destroy(vrhip_ctx *ctx);

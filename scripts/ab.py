@@ -4,7 +4,8 @@
   python scripts/ab.py [--cfg C2] [--frames 8] [--steps 4] lib1.so lib2.so ...
 
 Prints Mpaths/s per variant (median of 3 batches of back-to-back steps) and checks every variant's
-accumulation buffer bit-equals the first one's.
+accumulation buffer bit-equals the first one's (SHA-256 of the
+float4 bytes; one-frame calls too with --interactive).
 """
 import argparse
 import json
@@ -15,7 +16,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r"""
-import sys, time, json, numpy as np
+import sys, time, json, hashlib, numpy as np
 sys.path.insert(0, {repo!r})
 import torch
 from vrenderer_pathtracer_amd import VRendererHIP, scenes
@@ -54,11 +55,11 @@ if {inter} > 0:      # one frame per synchronous call (the reference's render() 
     ti.sort()
     inter = ti[1] * 1e3
     iacc = r.read_accum()
-    ihash = int(np.bitwise_xor.reduce(iacc.view(np.uint32).reshape(-1)))
+    ihash = hashlib.sha256(iacc.tobytes()).hexdigest()
 else:
-    ihash = 0
+    ihash = ""
 print(json.dumps({{"mpaths": paths / med / 1e6, "best": paths / ts[0] / 1e6, "inter_ms": inter,
-                   "hash": int(np.bitwise_xor.reduce(acc.view(np.uint32).reshape(-1))), "ihash": ihash}}))
+                   "hash": hashlib.sha256(acc.tobytes()).hexdigest(), "ihash": ihash}}))
 """
 
 
@@ -96,9 +97,9 @@ def main():
         name = os.path.basename(lib) + (f"@{envs}" if envs else "") + (f" overlap={ov}" if ov else "")
         results[name] = res
         it = f"  one frame/call {res['inter_ms']:.4f} ms" if res.get("inter_ms") else ""
-        print(f"{name:40s} {res['mpaths']:9.1f} Mpaths/s (best {res['best']:.1f}){it}  hash {res['hash']:#x}",
+        print(f"{name:40s} {res['mpaths']:9.1f} Mpaths/s (best {res['best']:.1f}){it}  sha256 {res['hash'][:16]}",
               flush=True)
-    hashes = {(v["hash"], v.get("ihash", 0)) for v in results.values()}
+    hashes = {(v["hash"], v.get("ihash", "")) for v in results.values()}
     print("all results identical" if len(hashes) == 1 else f"RESULTS DIFFER: {len(hashes)} distinct hashes")
 
 

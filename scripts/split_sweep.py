@@ -5,6 +5,7 @@ pass); larger splits store per-path results and sum them in the finish pass.
 
   python scripts/split_sweep.py [C4] [frames] [splits, e.g. 1,2,4,8,0]
 """
+import hashlib
 import os
 import sys
 import time
@@ -30,7 +31,7 @@ for sp in splits:
     r.clearBuffer()
     r.render(frames=F, times=[sc["time"] + k for k in range(F)])
     acc = r.read_accum()
-    h = int(np.bitwise_xor.reduce(acc.view(np.uint32).reshape(-1)))
+    h = hashlib.sha256(acc.tobytes()).hexdigest()
     ref = h if ref is None else ref
     for i in range(2):
         r.render(frames=F, times=[sc["time"] + (1 + i) * F + k for k in range(F)], sync=False)

@@ -27,7 +27,21 @@ def test_library_exports_every_header_symbol(native):
     declared = set(_native.header_symbols())
     assert declared, "no symbols parsed from include/vrhip.h"
     assert declared <= exported, sorted(declared - exported)
-    assert native.vrhip_abi_version() == 3
+    assert native.vrhip_abi_version() == 4
+
+
+def test_build_id_ties_library_to_sources(native):
+    """The library embeds the SHA-256 of the sources, include/vrhip.h and the
+    compile flags (vrhip_build_id); it equals the hash of the files on disk,
+    and the loader's staleness check reads it from the file itself."""
+    from vrenderer_pathtracer_amd import build
+    bid = native.vrhip_build_id().decode()
+    assert re.fullmatch(r"[0-9a-f]{64}", bid), bid
+    assert bid == build.source_id() == build.lib_build_id(LIB_PATH)
+    assert not build.needs_build()
+    assert _native.build_id()["matches_sources"]
+    # any change to a source or flag changes the id
+    assert build.source_id(["-DVR_SOMETHING=1"]) != bid
 
 
 def _has_gpu(native):

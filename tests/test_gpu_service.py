@@ -155,18 +155,23 @@ def test_service_kernel_stats_count_every_launch(native):
 
 
 @pytest.mark.parametrize("cfg,calls,frames", [
+    ("C2", 4, 16),      # THE HEADLINE PATH: 1280x720 Cornell + knot on the 7-wave Cornell service kernel, bench cadence
     ("C3", 4, 16),      # 1280x720: 4 back-to-back 16-frame launches, 32 paths per slot, pixel list beyond 1,024 runs
     ("C5", 2, 16),      # 3840x2160 1M-triangle knot: 2 launches of 66 M paths, 64 queue heads
 ])
 def test_service_session_full_size_equals_launch_by_launch(native, oracle, cfg, calls, frames):
-    """The render-service path that produces the C3 / C5 bench numbers, at the
+    """The render-service path that produces the bench numbers, at the
     BASELINE size and cadence: `calls` back-to-back async 16-frame calls in
-    ONE session (service mode 1) equal the same calls launch by launch
-    (service mode 0) bit for bit -- accum, RGBA8, depth -- so the session's
-    slot layout, its multi-slot finish pass and the listed-pixel runs are
-    exercised at full scale.  C5 also checks the session's image against the
-    glibc oracle over a 48-row band of the 4K frame (the tolerance of
-    test_gpu_parity's baseline-size test, over all the session's frames)."""
+    ONE session (service mode 1: one session, every launch taken by it) equal
+    the same calls launch by launch (service mode 0) bit for bit -- accum,
+    RGBA8, depth -- so the session's 16-frame slots (32 paths per slot), its
+    multi-slot finish pass, the XCD queue bands beyond the first (3,600
+    sub-tiles at 720p against 128 per band) and the listed-pixel runs are
+    exercised at full scale.  C2 (bench.py's workload, on the kernel the
+    bench times) is also compared with the portable-libm oracle over the
+    whole frame and all 64 frames, bit for bit.  C5 checks the session's image
+    against the glibc oracle over a 48-row band of the 4K frame (the tolerance
+    of test_gpu_parity's baseline-size test, over all the session's frames)."""
     sc = scenes.make_scene(cfg)
 
     def run(service):
@@ -179,13 +184,27 @@ def test_service_session_full_size_equals_launch_by_launch(native, oracle, cfg, 
             r.render(frames=frames, times=[t + frames * i + k for k in range(frames)], sync=False)
             kinds.append(r.last_launch_info()["kind"])
         out = r.read_accum(), r.read_rgba8(), r.read_depth8(), r.getFrameCount()
+        info = r.service_info()
         r.cleanUp()
-        return out, kinds
-    (a1, r1, d1, n1), k1 = run(1)
-    (a0, r0, d0, n0), k0 = run(0)
+        return out, kinds, info
+    (a1, r1, d1, n1), k1, i1 = run(1)
+    (a0, r0, d0, n0), k0, i0 = run(0)
     assert set(k1) == {"service"} and "service" not in k0, (k1, k0)
+    assert i1["sessions"] == 1 and i1["served"] == calls and i1["refused"] == 0, i1
+    assert i0["sessions"] == 0, i0
     assert n1 == n0 == calls * frames
     _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8"); _eq(d1, d0, "depth8")
+    if cfg == "C2":
+        nf = calls * frames
+        t0 = time.perf_counter()
+        oa, orgba, od, _ = po.render(sc, frames=nf, times=[sc["time"] + k for k in range(nf)],
+                                     libm=po.LIBM_PORTABLE)
+        print(f"C2 oracle, whole 1280x720 frame x {nf} frames: {time.perf_counter() - t0:.1f} s")
+        H, W = (sc["height"] // 16) * 16, (sc["width"] // 16) * 16
+        assert np.any(oa[:H, :W, :3] != 0)
+        _eq(a1[:H, :W], oa[:H, :W], "C2 session accum vs oracle")
+        _eq(r1[:H, :W], orgba[:H, :W], "C2 session rgba8 vs oracle")
+        _eq(d1[:H, :W], od[:H, :W], "C2 session depth8 vs oracle")
     if cfg == "C5":
         TOL_RMSE, TOL_PIX_FRAC = 1e-3, 0.995      # test_gpu_parity.py's north-star tolerance
         r0_, r1_ = 1056, 1104
@@ -206,10 +225,12 @@ def test_service_session_full_size_equals_launch_by_launch(native, oracle, cfg, 
 def test_service_retire_race_forced(native):
     """The lost-launch race, forced: the session kernel retires after 1 ms
     without a launch, the host's post window is 50 ms and the host sleeps 3 ms
-    between that window check and every post, so posts meet a retiring
+    between that window check and every post after a session's first, so
+    each session serves its first launch and the next post meets a retiring
     kernel.  The store-fence-load hand-shake must hand each such launch to the
     launch path (counted by vrhip_service_stats), the consumed-count check at
-    sync must pass, and the image must equal launch-by-launch rendering."""
+    sync must pass, and the image must equal launch-by-launch rendering --
+    with launches served by sessions and others refused, in one run."""
     sc = scenes.make_scene("C3", 96, 64)
     calls = [2, 1, 3, 2, 1, 2]
 
@@ -226,13 +247,51 @@ def test_service_retire_race_forced(native):
         r.sync()
         out = r.read_accum(), r.read_rgba8(), r.read_depth8(), r.getFrameCount()
         refused = r.service_refused()
+        info = r.service_info()
         r.cleanUp()
-        return out, refused
-    (a1, r1, d1, n1), refused = run(1, (1000, 50000, 3000))
-    (a0, r0, d0, n0), none = run(0, None)
+        return out, refused, info
+    (a1, r1, d1, n1), refused, info = run(1, (1000, 50000, 3000))
+    (a0, r0, d0, n0), none, _ = run(0, None)
     assert refused >= 1 and none == 0, (refused, none)
+    assert info["refused"] == refused and info["served"] >= 1, info
+    assert info["served"] + info["refused"] == len(calls), info
     assert n1 == n0 == sum(calls)
     _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8"); _eq(d1, d0, "depth8")
+
+
+def test_service_gather_not_deferred_in_automatic_mode(native):
+    """The deferred-gather foot-gun is gone from the default mode: in
+    automatic service mode a vrhip_comm_gather inside a session closes the
+    session and is enqueued at once (vrhip_service_info: no deferred gather),
+    while explicit mode 1 still defers; both give the launch-by-launch image.
+    One-rank RCCL communicator, back-to-back 16-frame C3 calls (each behind a
+    launch in flight, so automatic mode opens sessions)."""
+    from vrenderer_pathtracer_amd.renderer import comm_unique_id
+    from vrenderer_pathtracer_amd.tiles import WHAT_RGBA8
+    sc = scenes.make_scene("C3")
+
+    def run(service):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_service(service)
+        r.comm_init(0, 1, comm_unique_id())
+        t = sc["time"]
+        for i in range(4):
+            r.render(frames=16, times=[t + 16 * i + k for k in range(16)], sync=False)
+            r.comm_gather(WHAT_RGBA8)
+        r.sync()
+        out = r.read_accum(), r.read_rgba8()
+        info = r.service_info()
+        r.comm_destroy()
+        r.cleanUp()
+        return out, info
+    (aa, ar), ia = run(-1)
+    (ea, er), ie = run(1)
+    (ba, br), _ = run(0)
+    assert ia["sessions"] >= 1 and ia["deferred_gathers"] == 0, ia
+    assert ie["deferred_gathers"] >= 1, ie
+    for g in ((aa, ar), (ea, er)):
+        _eq(g[0], ba, "accum"); _eq(g[1], br, "rgba8")
 
 
 @pytest.mark.parametrize("mode", [-1, 1])

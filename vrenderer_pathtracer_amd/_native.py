@@ -34,6 +34,8 @@ ERRORS = {-1: "VRHIP_ERR_INVALID", -2: "VRHIP_ERR_HIP", -3: "VRHIP_ERR_NO_ENV", 
 _SIGNATURES = {
     "vrhip_last_error": (ctypes.c_char_p, []),
     "vrhip_abi_version": (ctypes.c_int, []),
+    "vrhip_build_id": (ctypes.c_char_p, []),
+    "vrhip_service_info": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_uint64)]),
     "vrhip_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "vrhip_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_ctx)]),
     "vrhip_destroy": (ctypes.c_int, [_ctx]),
@@ -128,6 +130,10 @@ def lib():
     global _lib
     if _lib is None:
         path = os.environ.get("VRHIP_LIB", _build.LIB_PATH)   # VRHIP_LIB: A/B builds of the same ABI
+        if path == _build.LIB_PATH and os.path.exists(path) and _build.needs_build():
+            # built from other sources than those on disk (its embedded
+            # vrhip_build_id differs): rebuild so what runs is what is checked in
+            _build.build()
         if not os.path.exists(path):
             raise RuntimeError(f"libvrhip.so not built ({path}); run vrenderer_pathtracer_amd.build.build()")
         L = ctypes.CDLL(path)
@@ -139,6 +145,15 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def build_id() -> dict:
+    """The loaded library's embedded build id (vrhip_build_id) and whether it
+    equals the SHA-256 of the sources and flags on disk."""
+    got = lib().vrhip_build_id().decode()
+    path = os.environ.get("VRHIP_LIB", _build.LIB_PATH)
+    return {"build_id": got, "matches_sources": got == _build.source_id(),
+            "lib": os.path.relpath(path, _build.REPO_DIR)}
 
 
 def check(code: int, where: str) -> None:

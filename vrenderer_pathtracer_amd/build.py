@@ -5,6 +5,7 @@ with ctypes.  Built in-tree so it travels with the repository snapshot.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -17,8 +18,9 @@ LIB_PATH = os.path.join(PKG_DIR, "libvrhip.so")
 # the path kernels' scene specialisations are separate translation units
 # (vr_spec_*.hip) so that they compile in parallel
 SOURCES = ["vr_spec_generic.hip", "vr_cls_cornell_mesh.hip", "vr_cls_hdri_mesh.hip", "vr_spec_c2.hip", "vr_spec_c3.hip", "vr_spec_c5.hip", "vr_spec_c1.hip",
-           "vr_spec_c4.hip", "vr_cls_sphere.hip", "vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp", "vr_exr.cpp"]
-HEADERS = ["vr_params.hpp", "vr_math.hpp", "vr_bvh.hpp", "vr_exr.hpp", "vr_kernel.hpp"]
+           "vr_spec_c4.hip", "vr_cls_sphere.hip", "vr_kernel.hip", "vrhip_api.cpp", "vr_bvh.cpp", "vr_exr.cpp",
+           "vr_merl.cpp"]
+HEADERS = ["vr_params.hpp", "vr_math.hpp", "vr_bvh.hpp", "vr_exr.hpp", "vr_merl.hpp", "vr_kernel.hpp"]
 ARCH = os.environ.get("VRHIP_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: results are defined without FMA contraction (parity
@@ -39,15 +41,43 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: cannot build libvrhip.so")
 
 
-def _newest_input_mtime() -> float:
-    paths = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    paths.append(os.path.join(REPO_DIR, "include", "vrhip.h"))
-    paths.append(os.path.abspath(__file__))
-    return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
+BUILD_ID_TAG = b"vrhip-build-id:"
+
+
+def source_id(extra_flags=None) -> str:
+    """SHA-256 of everything the library is compiled from: every source and
+    header (by name and content), include/vrhip.h, and the compile flags.
+    Embedded in the library (vrhip_build_id) so that a loaded or timed
+    library can be tied to the sources on disk."""
+    h = hashlib.sha256()
+    for name in sorted(SOURCES + HEADERS):
+        h.update(name.encode() + b"\0")
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(f.read())
+    with open(os.path.join(REPO_DIR, "include", "vrhip.h"), "rb") as f:
+        h.update(b"vrhip.h\0" + f.read())
+    h.update(" ".join(HIPCC_FLAGS + list(extra_flags or [])).encode())
+    return h.hexdigest()
+
+
+def lib_build_id(path: str = LIB_PATH):
+    """The build id embedded in a built library file (without loading it), or None."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(BUILD_ID_TAG)
+    if i < 0:
+        return None
+    hexid = data[i + len(BUILD_ID_TAG):i + len(BUILD_ID_TAG) + 64]
+    return hexid.decode("ascii", "replace")
 
 
 def needs_build() -> bool:
-    return not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < _newest_input_mtime()
+    """The library is missing or was built from other sources / flags than
+    those on disk (content hash, not modification times)."""
+    return lib_build_id(LIB_PATH) != source_id()
 
 
 def _jobs() -> int:
@@ -68,7 +98,9 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None, out_path
     import concurrent.futures
     import tempfile
     hipcc = _hipcc()
-    compile_flags = [f for f in HIPCC_FLAGS if f != "-shared"] + list(extra_flags or [])
+    bid = source_id(extra_flags)
+    compile_flags = ([f for f in HIPCC_FLAGS if f != "-shared"] + list(extra_flags or [])
+                     + [f'-DVRHIP_BUILD_ID="{BUILD_ID_TAG.decode()}{bid}"'])
     with tempfile.TemporaryDirectory(prefix="vrhip_build_") as tmpd:
         objs = [os.path.join(tmpd, os.path.splitext(s)[0] + ".o") for s in SOURCES]
 

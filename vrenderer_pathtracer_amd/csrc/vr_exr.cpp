@@ -162,13 +162,20 @@ int read_exr_rgba_half(const char* path, std::vector<uint16_t>& rgba, uint32_t& 
                 chans.push_back(c);
             }
         } else if (name == "compression") {
+            if (size < 1) { why = "bad compression attribute"; return -1; }
             compression = b[pos];
         } else if (name == "dataWindow" && type == "box2i") {
+            if (size < 16) { why = "bad dataWindow attribute"; return -1; }
             std::memcpy(dw, &b[pos], 16);
         }
         pos = end;
     }
     if (chans.empty() || compression < 0 || dw[2] < dw[0] || dw[3] < dw[1]) { why = "missing channels, compression or data window"; return -1; }
+    // the data window's size in 64-bit arithmetic (corner coordinates span
+    // the int32 range), bounded like the renderer's images: at most 65536 on
+    // a side and 2^28 pixels -- a corrupt header must not ask for terabytes
+    const int64_t w64 = (int64_t)dw[2] - (int64_t)dw[0] + 1, h64 = (int64_t)dw[3] - (int64_t)dw[1] + 1;
+    if (w64 > 65536 || h64 > 65536 || w64 * h64 > ((int64_t)1 << 28)) { why = "data window too large"; return -1; }
     int lines_per_block;
     switch (compression) {
     case 0: case 1: case 2: lines_per_block = 1; break;   // NONE, RLE, ZIPS
@@ -200,8 +207,9 @@ int read_exr_rgba_half(const char* path, std::vector<uint16_t>& rgba, uint32_t& 
             why = "truncated scanline chunk";
             return -1;
         }
-        const int32_t ly0 = y0 - dw[1];
-        if (ly0 < 0 || (uint32_t)ly0 >= height) { why = "scanline chunk outside the data window"; return -1; }
+        const int64_t ly64 = (int64_t)y0 - (int64_t)dw[1];
+        if (ly64 < 0 || ly64 >= (int64_t)height) { why = "scanline chunk outside the data window"; return -1; }
+        const int32_t ly0 = (int32_t)ly64;
         const uint32_t lines = std::min<uint32_t>((uint32_t)lines_per_block, height - (uint32_t)ly0);
         const size_t expect = line_bytes * lines;
         const uint8_t* src = &b[q];

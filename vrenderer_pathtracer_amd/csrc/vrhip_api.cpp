@@ -28,6 +28,7 @@
 #include "../../include/vrhip.h"
 #include "vr_bvh.hpp"
 #include "vr_exr.hpp"
+#include "vr_merl.hpp"
 #include "vr_params.hpp"
 
 using vr::vr3;
@@ -203,6 +204,9 @@ struct vrhip_ctx {
     // and the post (forces the retire-vs-post race)
     uint32_t svc_idle_us = 0, svc_window_us = 0, svc_post_delay_us = 0;
     uint64_t svc_refused = 0;                     // launches a retiring session kernel did not take
+    // vrhip_service_info: sessions opened, launches they took, gathers deferred
+    // to a session's close, sessions the scratch allocation could not open
+    uint64_t svc_sessions = 0, svc_served = 0, svc_deferred = 0, svc_alloc_fallbacks = 0;
     size_t svc_budget = 0;                        // vrhip_set_service_budget (0: VRHIP_SERVICE_BYTES / 24 GiB)
     // multi-device renderer (vrhip_create_multi): the lead context holds every
     // member context (itself first); settings fan out to all of them
@@ -532,6 +536,19 @@ extern "C" {
 const char* vrhip_last_error(void) { return g_last_error.c_str(); }
 int vrhip_abi_version(void) { return VRHIP_ABI_VERSION; }
 
+// SHA-256 of the sources, include/vrhip.h and the compile flags this library
+// was built from, tagged so build.py can read it from the file without
+// loading it (vrenderer_pathtracer_amd/build.py passes it in)
+#ifndef VRHIP_BUILD_ID
+#define VRHIP_BUILD_ID "vrhip-build-id:unknown"
+#endif
+const char* vrhip_build_id(void)
+{
+    static const char id[] = VRHIP_BUILD_ID;
+    static const char tag[] = "vrhip-build-id:";
+    return std::strncmp(id, tag, sizeof(tag) - 1) == 0 ? id + sizeof(tag) - 1 : id;
+}
+
 int vrhip_device_count(int* count)
 {
     if (!count) return fail(VRHIP_ERR_INVALID, "count is NULL");
@@ -800,18 +817,10 @@ static int one_upload_brdf(vrhip_ctx* c, const float* table, size_t n_floats)
 
 int vrhip_load_merl(const char* path, float* table, size_t n_floats)
 {
-    const size_t n = 90u * 90u * 360u / 2u;
-    if (!path || !table || n_floats != 3 * n) return fail(VRHIP_ERR_INVALID, "BRDF table must hold 3*1458000 floats");
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return fail(VRHIP_ERR_INVALID, std::string("cannot open ") + path);
-    int32_t dims[3] = { 0, 0, 0 };
-    f.read(reinterpret_cast<char*>(dims), sizeof(dims));
-    if (!f || (size_t)dims[0] * (size_t)dims[1] * (size_t)dims[2] != n)
-        return fail(VRHIP_ERR_INVALID, "MERL dimensions don't match 90x90x180");
-    std::vector<double> d(3 * n);
-    f.read(reinterpret_cast<char*>(d.data()), (std::streamsize)(3 * n * sizeof(double)));
-    if (!f) return fail(VRHIP_ERR_INVALID, "truncated MERL file");
-    for (size_t i = 0; i < 3 * n; ++i) table[i] = (float)d[i];
+    if (!path || !table || n_floats != vr::kMerlFloats)
+        return fail(VRHIP_ERR_INVALID, "BRDF table must hold 3*1458000 floats");
+    std::string why;
+    if (vr::read_merl(path, table, why) != 0) return fail(VRHIP_ERR_INVALID, why);
     return VRHIP_OK;
 }
 
@@ -1145,10 +1154,15 @@ static int svc_close(vrhip_ctx* c)
     S.ring_checked[S.cur_ring] = false;
     HIP_TRY(hipStreamWaitEvent(c->stream, S.k1, 0));
     // the launches the host posted and the kernel took (svc_post): a launch
-    // that met a retiring kernel was not counted and went the launch path
+    // that met a retiring kernel was not counted and went the launch path.
+    // A session that took none has nothing to sum: no finish pass (on a fresh
+    // accumulation it would tonemap with a frame count of 0) and no gathers
+    // (a gather is deferred only behind a launch the session took)
     S.fin.n = S.posted;
-    const int e = vr::launch_service_finish(S.p, S.fin, S.n_tiles, c->stream);
-    if (e != 0) return fail(VRHIP_ERR_HIP, std::string("service finish launch: ") + hipGetErrorString((hipError_t)e));
+    if (S.posted > 0) {
+        const int e = vr::launch_service_finish(S.p, S.fin, S.n_tiles, c->stream);
+        if (e != 0) return fail(VRHIP_ERR_HIP, std::string("service finish launch: ") + hipGetErrorString((hipError_t)e));
+    }
     // deferred gathers, in call order; rank 0 keeps its own tiles from the
     // finish pass (the final state) and unpacks the other ranks' of every gather
     for (const auto& g : S.gathers) {
@@ -1209,10 +1223,21 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     }
     const size_t stride = p.path_stride;
     size_t slot_bytes = 0;
-    const uint32_t slots = svc_slots(c, p.path_stride, kmax, &slot_bytes);
-    if (slots < 2) return fail(VRHIP_ERR_NOMEM, "render service: the budget holds fewer than 2 launch slots");
+    uint32_t slots = svc_slots(c, p.path_stride, kmax, &slot_bytes);
     const uint32_t stage_px = owned_tiles_of(c->W, c->H, 0, c->nranks) * 256u;   // rank 0 owns the most tiles
     const size_t stage_bytes = (24u * (size_t)stage_px + 255u) & ~(size_t)255u;
+    // the slots' scratch grows into at most half of the device memory free
+    // now (plus what the session already holds): several contexts or ranks
+    // on one GPU share it, and the launch path needs its own scratch
+    if (slots >= 2 && (size_t)slots * slot_bytes > S.scratch_cap) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const size_t avail = (free_b + S.scratch_cap + S.staging_cap) / 2u;
+            slots = (uint32_t)std::min<size_t>(slots, avail / (slot_bytes + stage_bytes));
+        }
+        (void)hipGetLastError();
+    }
+    if (slots < 2) return fail(VRHIP_ERR_NOMEM, "render service: device memory holds fewer than 2 launch slots");
     auto grow = [&](auto*& ptr, size_t& cap, size_t need) -> int {
         if (need <= cap) return VRHIP_OK;
         // the previous session's kernel and finish pass may still use the old buffer
@@ -1220,7 +1245,12 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
         if (S.finished_used) HIP_TRY(hipEventSynchronize(S.finished));
         dfree(ptr);
         cap = 0;
-        HIP_TRY(hipMalloc((void**)&ptr, need));
+        const hipError_t e = hipMalloc((void**)&ptr, need);
+        if (e != hipSuccess) {
+            ptr = nullptr;
+            (void)hipGetLastError();
+            return fail(VRHIP_ERR_NOMEM, std::string("render service scratch: ") + hipGetErrorString(e));
+        }
         cap = need;
         return VRHIP_OK;
     };
@@ -1268,6 +1298,7 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     S.ring_checked[ri] = false;
     S.ring_posted[ri] = 0;
     S.open = true;
+    ++c->svc_sessions;
     S.last_post = std::chrono::steady_clock::now();
     return VRHIP_OK;
 }
@@ -1292,6 +1323,7 @@ static bool svc_post(vrhip_ctx* c, uint32_t k, const uint32_t* times, uint32_t t
     if (__atomic_load_n(&S.host->retired, __ATOMIC_SEQ_CST) != 0u) return false;
     S.fin.n_frames[S.posted] = k;
     ++S.posted;
+    ++c->svc_served;
     S.last_post = std::chrono::steady_clock::now();
     return true;
 }
@@ -1411,8 +1443,19 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             while (done < n_frames) {
                 const uint32_t k = std::min<uint32_t>(n_frames - done, (uint32_t)vr::kMaxFramesPerLaunch);
                 if (c->svc.open && !svc_fits(c, p, k) && (rc = svc_close(c)) != VRHIP_OK) return rc;
-                if (!c->svc.open && (rc = svc_open(c, p, stack, n_tiles, k_max)) != VRHIP_OK) return rc;
-                if (c->svc_post_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(c->svc_post_delay_us));
+                if (!c->svc.open && (rc = svc_open(c, p, stack, n_tiles, k_max)) != VRHIP_OK) {
+                    // no scratch for the session's slots (memory shared with
+                    // other contexts or ranks): this call's remaining frames
+                    // take the launch path, which needs one launch's scratch
+                    if (rc != VRHIP_ERR_NOMEM) return rc;
+                    ++c->svc_alloc_fallbacks;
+                    refused = true;
+                    break;
+                }
+                // (the test hook's delay: only before posts after a session's
+                // first -- the first post meets a kernel that just started)
+                if (c->svc_post_delay_us && c->svc.posted > 0)
+                    std::this_thread::sleep_for(std::chrono::microseconds(c->svc_post_delay_us));
                 if (!svc_post(c, k, times ? times + done : nullptr, time_seed)) {
                     // the session's kernel retired as this launch was posted:
                     // close the session without it; this call's remaining
@@ -1826,6 +1869,17 @@ int vrhip_service_stats(vrhip_ctx* c, uint64_t* refused_launches)
     return VRHIP_OK;
 }
 
+int vrhip_service_info(vrhip_ctx* c, uint64_t out[VRHIP_SERVICE_INFO])
+{
+    if (!c || !out) return fail(VRHIP_ERR_INVALID, "null argument");
+    out[0] = c->svc_refused;
+    out[1] = c->svc_sessions;
+    out[2] = c->svc_served;
+    out[3] = c->svc_deferred;
+    out[4] = c->svc_alloc_fallbacks;
+    return VRHIP_OK;
+}
+
 static int one_set_path_split(vrhip_ctx* c, uint32_t groups)
 {
     if (!c || groups > 2u * vr::kMaxFramesPerLaunch) return fail(VRHIP_ERR_INVALID, "bad path split");
@@ -1939,11 +1993,16 @@ int vrhip_comm_gather(vrhip_ctx* c, int what)
     if (!c || what < 0 || what > 2) return fail(VRHIP_ERR_INVALID, "bad gather arguments");
     if (!c->comm) return fail(VRHIP_ERR_INVALID, "vrhip_comm_init has not been called");
     int rc = set_device(c); if (rc) return rc;
-    if (c->svc.open && c->svc.posted > 0) {
-        // inside a session: the image after its last launch is staged by the
-        // session's finish pass and gathered when the session closes
+    if (c->service > 0 && c->svc.open && c->svc.posted > 0) {
+        // explicit service mode only: inside a session the image after its
+        // last launch is staged by the session's finish pass and gathered
+        // when the session closes (the caller syncs before any host-side
+        // wait on the other ranks, include/vrhip.h).  In automatic mode the
+        // gather closes the session and is enqueued now (below, through
+        // vrhip_pack_tiles), so no rank's collective waits on a host call
         c->svc.fin.gather[c->svc.posted - 1u] |= 1u << what;
         c->svc.gathers.emplace_back(c->svc.posted - 1u, what);
+        ++c->svc_deferred;
         return VRHIP_OK;
     }
     // pack -> gather -> (rank 0) unpack, all on the context stream, behind the

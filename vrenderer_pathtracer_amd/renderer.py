@@ -382,6 +382,13 @@ class VRendererHIP:
         check(self._lib.vrhip_service_stats(self._need_ctx(), ctypes.byref(n)), "vrhip_service_stats")
         return int(n.value)
 
+    def service_info(self) -> dict:
+        """Render-service counts since creation (vrhip_service_info)."""
+        c = (ctypes.c_uint64 * 5)()
+        check(self._lib.vrhip_service_info(self._need_ctx(), c), "vrhip_service_info")
+        return {"refused": int(c[0]), "sessions": int(c[1]), "served": int(c[2]), "deferred_gathers": int(c[3]),
+                "alloc_fallbacks": int(c[4])}
+
     def owned_pixels(self) -> int:
         """Pixels this rank renders (256 per owned 16x16 tile)."""
         n = ctypes.c_uint32(0)
