@@ -218,6 +218,56 @@ def test_multi_context_service_burst_bitexact(native, cfg, service):
     assert np.array_equal(gr, sr) and np.array_equal(gd, sd)
 
 
+@pytest.mark.parametrize("cfg", ["C4", "C5"])
+def test_eight_tile_ranks_full_size_reassemble_bitexact(native, cfg):
+    """The driver's 8-GPU configurations rehearsed on one GPU at full size:
+    C4 (1920x1080, MERL sphere) and C5 (3840x2160, 1M-triangle knot) rendered
+    as 8 tile ranks (set_tiling(r, 8), r = 0..7, each from a cleared
+    accumulation), every rank's RGBA8 / float4 accumulation / depth tiles
+    packed on the device (vrhip_pack_tiles) into one rank-major gather buffer
+    -- the layout ncclGather hands rank 0 -- then scattered back
+    (vrhip_unpack_tiles): accum, RGBA8 and depth equal the single-context
+    render of the whole image bit for bit."""
+    import torch
+    from vrenderer_pathtracer_amd import VRendererHIP, scenes
+    from vrenderer_pathtracer_amd.tiles import WHAT_ACCUM, WHAT_DEPTH8, WHAT_RGBA8, max_owned_pixels
+    sc = scenes.make_scene(cfg)
+    W, H = sc["width"], sc["height"]
+    n, frames = 8, 2
+    times = [sc["time"] + 3, sc["time"] + 4]
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.render(frames=frames, times=times)
+    ref = r.read_accum(), r.read_rgba8(), r.read_depth8()
+    whats = (WHAT_RGBA8, WHAT_ACCUM, WHAT_DEPTH8)
+    esz = {WHAT_RGBA8: 4, WHAT_ACCUM: 16, WHAT_DEPTH8: 4}
+    stride = {w: max_owned_pixels(W, H, n) * esz[w] for w in whats}
+    bufs = {w: torch.empty(n * stride[w], dtype=torch.uint8, device="cuda:0") for w in whats}
+    owned = []
+    for rank in range(n):
+        r.set_tiling(rank, n)
+        r.clearBuffer()
+        r.render(frames=frames, times=times)
+        owned.append(r.owned_pixels())
+        for w in whats:
+            r.pack_tiles(w, bufs[w].data_ptr() + rank * stride[w])
+        r.sync()
+    assert sum(owned) == (W // 16) * (H // 16) * 256
+    r.set_tiling(0, 1)
+    r.clearBuffer()                            # the gathering rank's images hold nothing of their own
+    for w in whats:
+        r.unpack_tiles(w, bufs[w].data_ptr(), n, stride[w])
+    got = r.read_accum(), r.read_rgba8(), r.read_depth8()
+    r.cleanUp()
+    hr = (H // 16) * 16
+    for g, e, what in zip(got, ref, ("accum", "rgba8", "depth8")):
+        g, e = g[:hr], e[:hr]
+        if g.dtype == np.float32:
+            g, e = g.view(np.uint32), e.view(np.uint32)
+        assert np.any(e != 0), what
+        assert np.array_equal(g, e), f"{cfg} {what}: {int((g != e).any(-1).sum())} pixels differ"
+
+
 def test_multi_context_two_devices_bitexact(native):
     """Two GPUs behind one context: each renders half the tiles, RCCL gathers
     them to the first; the images equal the one-GPU render bit for bit."""
