@@ -603,11 +603,15 @@ __device__ __forceinline__ void trav_finish(const Trav& tr, HitRec& hr)
 }
 
 template <int STACK, bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt)
+__device__ __forceinline__ void traverse_mesh(const RenderParams& p, const Ray& r, HitRec& hr, const Lds& L, Cnt& cnt,
+                                              bool any_hit = false)
 {
     Trav tr;
     trav_init<FEAT>(p, r, hr.t, tr, L);
-    while (tr.nodeAddr != kSentinel) trav_iter<STACK, COUNT, FEAT>(p, r, tr, L, cnt);
+    while (tr.nodeAddr != kSentinel) {
+        trav_iter<STACK, COUNT, FEAT>(p, r, tr, L, cnt);
+        if (any_hit && tr.best >= 0) tr.nodeAddr = kSentinel;     // (any_hit_enough)
+    }
     trav_finish(tr, hr);
 }
 // intersectScene (PathTracer.cu:136-468): closest hit, attributes deferred.
@@ -771,6 +775,56 @@ __device__ __forceinline__ vr4 emission_of(const HitRec& hr) {
         return mk4(s.ex, s.ey, s.ez, 0.f);
     }
     return mk4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Whether the mesh must be traversed for a ray whose closest SPHERE hit is
+// `hr`, on bounce `bounce`.  On the last bounce (3) only the closest hit's
+// emission is observable (bounce_step adds mask * emission and ends the path;
+// the reference's material sampling after it, PathTracer.cu:663-764,
+// prepares a ray it never traces) -- or, for a ray that hits nothing, the
+// miss branch (the Cornell escape's 0, or the HDRI's radiance, :631-652).
+// The mesh's emission is exactly (+0, +0, +0, 0) (:454-462; fill_hit,
+// emission_of), and so is that of every sphere but the Cornell box's light
+// and its two coloured walls.  So when the closest sphere hit has that
+// emission, whether a triangle lies in front of it changes no bit of the
+// result (the same product with the same zero vector is added) and the
+// traversal is skipped.  A ray that hits no sphere, or an emitting one, is
+// traversed (the mesh decides between a miss and a hit, or occludes the
+// emitter).  Not in the reference-algorithm counting variant or the strict
+// walk, which keep the reference's work.  C2: the last bounce is a third of
+// the rays a path traces (+6 %, r06b).
+#ifndef VR_LAST_BOUNCE_SKIP
+#define VR_LAST_BOUNCE_SKIP 1         // 0: off, 1: skip + any-hit (below), 2: skip only (A/B builds)
+#endif
+#ifndef VR_LAST_BOUNCE_HDRI
+#define VR_LAST_BOUNCE_HDRI 1         // 0: the Cornell box only (A/B builds)
+#endif
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool last_bounce_opt(const RenderParams& p, int bounce)
+{
+    // (HDRI scenes: C3 +1 %, C5 +0.6 %, r06c; not the textured one-frame
+    // kernel, where it cost 5 spilled VGPRs)
+    constexpr bool TEX1 = (FEAT & F_INLINE_PRIM) != 0u && (FEAT & (F_TEX_DIFF | F_TEX_NORM | F_TEX_SPEC)) != 0u;
+    return VR_LAST_BOUNCE_SKIP != 0 && !ref_alg<COUNT, FEAT>() && !HAS(F_STRICT) && bounce == 3 &&
+           (HAS(F_CORNELL) || (VR_LAST_BOUNCE_HDRI != 0 && !TEX1));
+}
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool mesh_needed(const RenderParams& p, const HitRec& hr, int bounce)
+{
+    if (!last_bounce_opt<COUNT, FEAT>(p, bounce) || (hr.kind != HK_CORNELL && hr.kind != HK_SMALL)) return true;
+    const vr4 e = emission_of(hr);
+    return (__float_as_uint(e.x) | __float_as_uint(e.y) | __float_as_uint(e.z)) != 0u;
+}
+// The traversals that remain on that bounce (the closest sphere emits, or
+// none is hit) need only WHETHER a triangle lies closer than the sphere hit:
+// any triangle the walk accepts makes the hit a mesh hit, whose emission is
+// 0 whichever triangle it is.  So the walk may stop at the end of the outer
+// iteration in which it first accepts one (any-hit instead of closest-hit;
+// C2 a further +1.3 %, r06b).
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool any_hit_enough(const RenderParams& p, int bounce)
+{
+    return VR_LAST_BOUNCE_SKIP == 1 && last_bounce_opt<COUNT, FEAT>(p, bounce);
 }
 
 // MERL index maps (PathTracer.cu:473-506)
@@ -1110,8 +1164,8 @@ __device__ __forceinline__ vr4 trace(const RenderParams& p, Ray ray, const HitRe
             // jitter, PathTracer.cu:842-844): its hit is computed once per pixel
             hr = hr0;
             (void)hit0;
-        } else {
-            (void)intersect_scene<STACK, COUNT, FEAT>(p, ray, hr, L, cnt);
+        } else if (intersect_spheres<COUNT, FEAT>(p, ray, hr, cnt) && mesh_needed<COUNT, FEAT>(p, hr, ps.bounce)) {
+            traverse_mesh<STACK, COUNT, FEAT>(p, ray, hr, L, cnt, any_hit_enough<COUNT, FEAT>(p, ps.bounce));
         }
         vr4 out;
         if (bounce_step<COUNT, FEAT>(p, ray, hr, ps, out, cnt)) { depth = ps.depth; return out; }
@@ -1934,7 +1988,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
             }
         }
         if (state == LS_SETUP) {
-            if (intersect_spheres<CNT, FEAT>(p, ray, hr, cnt)) {
+            if (intersect_spheres<CNT, FEAT>(p, ray, hr, cnt) && mesh_needed<CNT, FEAT>(p, hr, ps.bounce)) {
                 trav_init<FEAT>(p, ray, hr.t, tr, L);
                 state = LS_TRAV;
             } else {
@@ -1956,6 +2010,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
                 }
                 if (state == LS_TRAV || state == LS_HELP) {
                     trav_iter<STACK, CNT, FEAT>(p, ray, tr, L, cnt);
+                    if (state == LS_TRAV && any_hit_enough<CNT, FEAT>(p, ps.bounce) && tr.best >= 0) tr.nodeAddr = kSentinel;
                     if (tr.nodeAddr == kSentinel) {
                         if (state == LS_HELP) {
                             state = LS_HELPDONE;           // its best hit waits for the owner (help_step)
@@ -2290,7 +2345,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
     // every lane idle (LS_DONE): the loop's refill waits for the first chunk
     for (;;) {
         if (state == LS_SETUP) {
-            if (intersect_spheres<false, FEAT>(p, ray, hr, cnt)) {
+            if (intersect_spheres<false, FEAT>(p, ray, hr, cnt) && mesh_needed<false, FEAT>(p, hr, ps.bounce)) {
                 trav_init<FEAT>(p, ray, hr.t, tr, L);
                 state = LS_TRAV;
             } else {
@@ -2306,6 +2361,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
                 if (cur_sub == ~0u && n_shade > 0 && n_shade * VR_DRAIN_SHADE_NUM >= n_trav * VR_DRAIN_SHADE_DEN) break;
                 if (state == LS_TRAV) {
                     trav_iter<STACK, false, FEAT>(p, ray, tr, L, cnt);
+                    if (any_hit_enough<false, FEAT>(p, ps.bounce) && tr.best >= 0) tr.nodeAddr = kSentinel;
                     if (tr.nodeAddr == kSentinel) {
                         trav_finish(tr, hr);
                         state = LS_SHADE;
