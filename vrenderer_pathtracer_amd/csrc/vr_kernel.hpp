@@ -416,6 +416,27 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     tr.nodeAddr = none ? top : nearc;
 }
 
+// The root visit at ray setup (path kernels).  Every lane that starts a walk
+// is at the root, so node_step's wave-uniform choice takes the block's LDS
+// copy of the tree top: the walk's first visit -- the same fetch of the same
+// node, the same slab tests, the same push and pop -- without the two global
+// loads and the round trip it cost inside trav_iter, and a ray that enters
+// neither child of the root (most Cornell-box bounce rays run wall to wall
+// past the mesh) leaves for shading at once instead of passing through the
+// traversal state machine.  The walk then resumes from the root's near child
+// exactly as it would have, so every lane's sequence of visits and tests is
+// unchanged.  false: the walk is over (no mesh hit).
+#ifndef VR_ROOT_AT_SETUP
+#define VR_ROOT_AT_SETUP 0
+#endif
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ bool root_visit(const RenderParams& p, const Ray& r, Trav& tr, const Lds& L, Cnt& cnt)
+{
+    if (VR_ROOT_AT_SETUP == 0 || L.n_cached < 1) return true;
+    node_step<COUNT, FEAT>(p, r, tr, L, cnt);
+    return tr.nodeAddr != kSentinel;
+}
+
 // Equal-t tie-break of the culled traversal.  The reference keeps the first
 // of two triangles hit at exactly the same distance (strict `<`,
 // PathTracer.cu:379), i.e. the one its depth-first walk tests first: slot
@@ -1990,7 +2011,7 @@ __device__ __forceinline__ void wave_body(const RenderParams& p, const Lds& L)
         if (state == LS_SETUP) {
             if (intersect_spheres<CNT, FEAT>(p, ray, hr, cnt) && mesh_needed<CNT, FEAT>(p, hr, ps.bounce)) {
                 trav_init<FEAT>(p, ray, hr.t, tr, L);
-                state = LS_TRAV;
+                state = root_visit<CNT, FEAT>(p, ray, tr, L, cnt) ? LS_TRAV : LS_SHADE;
             } else {
                 state = LS_SHADE;
             }
@@ -2347,7 +2368,7 @@ __device__ __forceinline__ void service_body(const RenderParams& p, const Lds& L
         if (state == LS_SETUP) {
             if (intersect_spheres<false, FEAT>(p, ray, hr, cnt) && mesh_needed<false, FEAT>(p, hr, ps.bounce)) {
                 trav_init<FEAT>(p, ray, hr.t, tr, L);
-                state = LS_TRAV;
+                state = root_visit<false, FEAT>(p, ray, tr, L, cnt) ? LS_TRAV : LS_SHADE;
             } else {
                 state = LS_SHADE;
             }
