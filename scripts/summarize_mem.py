@@ -57,21 +57,29 @@ def main():
     paths = int(sys.argv[4]) if len(sys.argv) > 4 else None
     per = defaultdict(list)
     kernels = set()
-    for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
+    files = glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")) + \
+        glob.glob(os.path.join(src, "valu*", "*counter_collection.csv"))      # scripts/gpu_valu.sh passes
+    for f in sorted(files):
         for r in csv.DictReader(open(f)):
             if production_wave(r["Kernel_Name"]):
                 kernels.add(r["Kernel_Name"].split("(")[0])
                 per[r["Counter_Name"]].append((int(r["Start_Timestamp"]), float(r["Counter_Value"]),
-                                               int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+                                               int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                                               "render_service_kernel" in r["Kernel_Name"]))
     m, dur = {}, {}
     svc = any("render_service_kernel" in k for k in kernels)
     for k, v in per.items():
         v.sort()
-        # a service run: its timed steps are the last dispatch (one session);
-        # the warmup step before it ran on the launch path
-        t = v[-1:] if svc else v[-TIMED:]
-        m[k] = sum(x for _, x, _ in t) / len(t)
-        dur[k] = sum(d for _, _, d in t) / len(t)
+        # a service run: its timed steps are the FIRST service dispatch (one
+        # session; the warmup step before it ran on the launch path, and
+        # bench.py's self-check after the timed loop renders one more session
+        # and launch-path steps)
+        if svc:
+            t = [x for x in v if x[3]][:1]
+        else:
+            t = [x for x in v if not x[3]][:TIMED + 1][-TIMED:]   # (warmup first, then the timed steps)
+        m[k] = sum(x[1] for x in t) / len(t)
+        dur[k] = sum(x[2] for x in t) / len(t)
     lines = [f"# Issue and memory-pipeline counters, {name} ({cfg})", "",
              f"Source: `scripts/gpu_mem.sh` (one counter group per rocprofv3 pass) on `bench.py --config {cfg}`; "
              f"means over the {TIMED} timed dispatches of the production kernel "
@@ -116,7 +124,18 @@ def main():
                 lines.append(f"- {label} wave-instructions per path: {m[k] / paths:.2f}")
     out = os.path.join(REPO, "profiles", f"{name}_mem.md")
     open(out, "w").write("\n".join(lines) + "\n")
-    if g:   # unit busy fractions for bench.py's roofline.unit_busy
+    f64 = sum(m.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                                        "SQ_INSTS_VALU_TRANS_F64"))
+    if f64 and m.get("SQ_INSTS_VALU"):
+        lines.append(f"- F64 VALU instructions (FMA + MUL + ADD + TRANS): {f64 / m['SQ_INSTS_VALU']:.3f} of all VALU")
+        for k in ("SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32",
+                  "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT"):
+            if k in m:
+                lines.append(f"- {k[14:]}: {m[k] / m['SQ_INSTS_VALU']:.3f} of all VALU")
+        if "SQ_INST_CYCLES_VALU" in m:
+            lines.append(f"- VALU issue cycles per VALU instruction (SQ_INST_CYCLES_VALU / SQ_INSTS_VALU): "
+                         f"{m['SQ_INST_CYCLES_VALU'] / m['SQ_INSTS_VALU']:.2f}")
+    if g and "TD_TD_BUSY_sum" in m:   # unit busy fractions for bench.py's roofline.unit_busy
         cyc = g / 8.0
         units = {"source": os.path.relpath(out, REPO)}
         for k, key in (("TD_TD_BUSY_sum", "td"), ("TA_TA_BUSY_sum", "ta")):

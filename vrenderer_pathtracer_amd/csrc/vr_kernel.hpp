@@ -317,6 +317,19 @@ __device__ __forceinline__ int trav_pop(Trav& tr, const Lds& L)
     return L.stk[(tr.sp--) * L.stride];
 }
 
+// Whether node visits may read the block's LDS copy of the tree top.  Off
+// (VR_SVC_LDS_NODES=0, A/B builds) in the Cornell-box service kernels: the
+// wave-uniform choice almost never finds a diverged wave entirely in the
+// cached top there (0.2 % of node bytes, r05), so the test per visit is spent
+// for nothing.
+#ifndef VR_SVC_LDS_NODES
+#define VR_SVC_LDS_NODES 1
+#endif
+template <uint32_t FEAT>
+constexpr bool lds_nodes_on() {
+    return VR_SVC_LDS_NODES != 0 || (FEAT & F_SERVICE) == 0u || (FEAT & F_CORNELL) == 0u;
+}
+
 // One inner-node visit (:295-343): fetch (LDS copy or L2/HBM), two slab
 // tests, near child next, far child pushed when both are entered, pop when
 // neither is.  Leaves in tr.nodeAddr are left to the caller.
@@ -333,7 +346,7 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     const int node = tr.nodeAddr >> 2;
     // wave-uniform choice between the LDS copy and L2/HBM: a diverged wave
     // would pay both round trips
-    const bool in_lds = __ballot(node >= L.n_cached) == 0ull;
+    const bool in_lds = lds_nodes_on<FEAT>() && __ballot(node >= L.n_cached) == 0ull;
     if (COUNT) {
         cnt.nodes_lds += in_lds ? 1u : 0u;
         if (!in_lds) { cnt.ld128 += strict ? 3u : 2u; cnt.ld64 += strict ? 1u : 0u; }
