@@ -384,7 +384,8 @@ int vrhip_kernel_stats(vrhip_ctx *ctx, double *total_ms, uint64_t *launches, int
  * reference counterpart): path groups per pixel (sphere-only scenes), whether
  * the paths' results went through the result scratch and the finish pass (1)
  * or were accumulated in registers in path order (0), and the kernel family
- * (0 render_kernel, 1 path-pool kernel, 2 render service). */
+ * (0 render_kernel, 1 path-pool kernel, 2 render service, 3 path-pool kernel
+ * + finish pass as one graph launch: VRHIP_GRAPH=1, one-frame calls). */
 int vrhip_last_launch_info(vrhip_ctx *ctx, uint32_t *split, uint32_t *use_scratch, uint32_t *kind);
 /* Vector-memory gather roof of `device` (the ceiling the path kernel's
  * node, triangle and attribute fetches run against; no reference

@@ -341,3 +341,46 @@ def test_service_4k_hdri_mesh_64_frame_calls(native):
         return out
     (a1, r1), (a0, r0) = run(-1), run(0)
     _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8")
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_one_frame_graph_equals_launches(native, oracle, cfg):
+    """VRHIP_GRAPH=1: synchronous one-frame calls (kernel timing off, the Qt
+    adapter's configuration) launch the path kernel + finish pass as one HIP
+    graph, captured per longest-first order slot and re-captured when the
+    launch changes (here: a Fresnel change and a clear mid-run).  Images equal
+    plain launches bit for bit and, for the first frames, the oracle."""
+    import os
+    sc = scenes.make_scene(cfg, 96, 64)
+
+    def run(graph):
+        old = os.environ.get("VRHIP_GRAPH")
+        os.environ["VRHIP_GRAPH"] = "1" if graph else "0"
+        try:
+            r = VRendererHIP(0)
+            scenes.load_into(r, sc)            # (init() creates the context, which reads VRHIP_GRAPH)
+        finally:
+            if old is None:
+                del os.environ["VRHIP_GRAPH"]
+            else:
+                os.environ["VRHIP_GRAPH"] = old
+        r.set_kernel_timing(False)
+        t = sc["time"]
+        kinds, snaps = [], []
+        for i in range(12):
+            if i == 6:
+                snaps.append(r.read_accum())
+                r.setFresnelCoef(0.3)          # another launch parameter (and a clear): a new capture
+            r.render(frames=1, times=[t + i], sync=True)
+            kinds.append(r.last_launch_info()["kind"])
+        out = r.read_accum(), r.read_rgba8(), r.read_depth8()
+        r.cleanUp()
+        return snaps + list(out), kinds
+    g, gk = run(True)
+    b, bk = run(False)
+    assert "path_pool_graph" in gk and "path_pool_graph" not in bk, (gk, bk)
+    for x, y, what in zip(g, b, ("accum@6", "accum", "rgba8", "depth8")):
+        _eq(x, y, what)
+    oa, _, _, _ = po.render(sc, frames=6, times=[sc["time"] + k for k in range(6)], libm=po.LIBM_PORTABLE)
+    H, W = (64 // 16) * 16, (96 // 16) * 16
+    _eq(g[0][:H, :W], oa[:H, :W], "graph accum@6 vs oracle")

@@ -211,6 +211,20 @@ struct vrhip_ctx {
     // multi-device renderer (vrhip_create_multi): the lead context holds every
     // member context (itself first); settings fan out to all of them
     std::vector<vrhip_ctx*> group;
+    // one-frame launches as a HIP graph (VRHIP_GRAPH=1; one_frame_graph): the
+    // path kernel + finish pass captured once per longest-first order slot,
+    // their kernel arguments updated per frame
+    struct FrameGraph {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t x = nullptr;
+        hipGraphNode_t kn[2] = { nullptr, nullptr };
+        hipKernelNodeParams kp[2] = {};
+        vr::RenderParams key{};               // the launch parameters except the frame's number and seed
+        vr::RenderParams arg{};               // this frame's parameters (the nodes' argument)
+        bool valid = false;
+    } fgraph[2];
+    bool use_graph = false;
+    uint64_t graph_launches = 0, graph_captures = 0;
     // the lead of a group: renders since the colour / depth tiles were last
     // gathered (the gather runs when the lead's images are next needed)
     bool group_stale = false;
@@ -573,6 +587,7 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     c->fov_scale = default_fov_scale();
     if (const char* e = std::getenv("VRHIP_COST_ORDER")) c->cost_order = std::atoi(e) != 0;
     if (const char* e = std::getenv("VRHIP_KERNEL_TIMING")) c->kernel_timing = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VRHIP_GRAPH")) c->use_graph = std::atoi(e) != 0;
     if (const char* e = std::getenv("VRHIP_SERVICE")) c->service = std::max(-1, std::min(1, std::atoi(e)));
     int rc;
     if ((rc = set_device(c)) != VRHIP_OK) { delete c; return rc; }
@@ -661,6 +676,10 @@ int vrhip_destroy(vrhip_ctx* c)
     svc_free(c);
     for (hipEvent_t e : c->kev_free) (void)hipEventDestroy(e);
     if (c->kev_origin) (void)hipEventDestroy(c->kev_origin);
+    for (auto& G : c->fgraph) {
+        if (G.x) (void)hipGraphExecDestroy(G.x);
+        if (G.g) (void)hipGraphDestroy(G.g);
+    }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return VRHIP_OK;
@@ -1340,6 +1359,63 @@ static bool svc_fits(const vrhip_ctx* c, const vr::RenderParams& p, uint32_t k)
     return std::memcmp(&key, &S.key, sizeof(key)) == 0;
 }
 
+// One-frame launches as a HIP graph (VRHIP_GRAPH=1, experiment): the path
+// kernel and the finish pass of a synchronous one-frame call, captured from
+// the context stream once per longest-first order slot (the slots' order and
+// cost buffers differ), re-captured when any launch parameter but the
+// frame's number and seed changes, and launched with those two kernel nodes'
+// arguments updated -- one graph launch instead of two kernel launches
+// between the host's wake-up and the next frame's path kernel.
+static int one_frame_graph(vrhip_ctx* c, const vr::RenderParams& p, uint32_t n_tiles, int stack, uint32_t gi)
+{
+    auto& G = c->fgraph[gi];
+    vr::RenderParams key = p;
+    key.first_frame = 0;
+    std::memset(key.times, 0, sizeof(key.times));
+    if (!G.valid || std::memcmp(&key, &G.key, sizeof(key)) != 0) {
+        if (G.x) { (void)hipGraphExecDestroy(G.x); G.x = nullptr; }
+        if (G.g) { (void)hipGraphDestroy(G.g); G.g = nullptr; }
+        G.valid = false;
+        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        const int e1 = vr::launch_render(p, n_tiles, stack, 0, c->stream);
+        const int e2 = vr::launch_finish(p, n_tiles, c->stream);
+        const hipError_t ec = hipStreamEndCapture(c->stream, &G.g);
+        if (e1 || e2 || ec != hipSuccess)
+            return fail(VRHIP_ERR_HIP, std::string("one-frame graph capture: ") +
+                                           hipGetErrorString(ec != hipSuccess ? ec : (hipError_t)(e1 ? e1 : e2)));
+        size_t n = 0;
+        HIP_TRY(hipGraphGetNodes(G.g, nullptr, &n));
+        std::vector<hipGraphNode_t> nodes(n);
+        HIP_TRY(hipGraphGetNodes(G.g, nodes.data(), &n));
+        int k = 0;
+        for (size_t i = 0; i < n; ++i) {
+            hipGraphNodeType t;
+            HIP_TRY(hipGraphNodeGetType(nodes[i], &t));
+            if (t != hipGraphNodeTypeKernel) continue;
+            if (k == 2) return fail(VRHIP_ERR_HIP, "one-frame graph: more than two kernel nodes");
+            G.kn[k] = nodes[i];
+            HIP_TRY(hipGraphKernelNodeGetParams(nodes[i], &G.kp[k]));
+            ++k;
+        }
+        if (k != 2) return fail(VRHIP_ERR_HIP, "one-frame graph: expected the path kernel and the finish pass");
+        HIP_TRY(hipGraphInstantiate(&G.x, G.g, nullptr, nullptr, 0));
+        G.key = key;
+        G.valid = true;
+        ++c->graph_captures;
+    }
+    G.arg = p;
+    void* args[1] = { &G.arg };
+    for (int k = 0; k < 2; ++k) {
+        hipKernelNodeParams kp = G.kp[k];
+        kp.kernelParams = args;
+        kp.extra = nullptr;
+        HIP_TRY(hipGraphExecKernelNodeSetParams(G.x, G.kn[k], &kp));
+    }
+    HIP_TRY(hipGraphLaunch(G.x, c->stream));
+    ++c->graph_launches;
+    return VRHIP_OK;
+}
+
 // count: 0 production, 1 reference-algorithm counting variant (in place, no
 // scratch), 2 instrumented production kernels (same launch shape as 0)
 static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, uint32_t time_seed, int count)
@@ -1602,15 +1678,25 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
             c->last_split = p.split; c->last_use_scratch = p.use_scratch;
             c->last_kind = wave_kernel ? 1u : 0u;
         }
-        int e = vr::launch_render(p, n_tiles, stack, count, rs);
-        if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
-        if (k1) HIP_TRY(hipEventRecord(k1, rs));
-        if (on_lane) {
-            HIP_TRY(hipEventRecord(l.done, rs));
-            HIP_TRY(hipStreamWaitEvent(c->stream, l.done, 0));
+        // a synchronous one-frame call's path kernel + finish pass as one graph launch (VRHIP_GRAPH)
+        const bool graph = c->use_graph && count == 0 && wave_kernel && k == 1u && !on_lane && rs == c->stream &&
+                           !k1 && p.inline_prim && p.use_scratch;
+        if (graph) {
+            const uint32_t gi = (p.sub_cost && p.sub_cost == l.sub_cost[1]) ? 1u : 0u;
+            if ((rc = one_frame_graph(c, p, n_tiles, stack, gi)) != VRHIP_OK) return rc;
+            c->last_kind = 3u;
+        } else {
+            int e = vr::launch_render(p, n_tiles, stack, count, rs);
+            if (e != 0) return fail(VRHIP_ERR_HIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
+            if (k1) HIP_TRY(hipEventRecord(k1, rs));
+            if (on_lane) {
+                HIP_TRY(hipEventRecord(l.done, rs));
+                HIP_TRY(hipStreamWaitEvent(c->stream, l.done, 0));
+            }
+            e = vr::launch_finish(p, n_tiles, c->stream);
+            if (e != 0) return fail(VRHIP_ERR_HIP, std::string("finish launch: ") + hipGetErrorString((hipError_t)e));
         }
-        e = vr::launch_finish(p, n_tiles, c->stream);
-        if (e != 0) return fail(VRHIP_ERR_HIP, std::string("finish launch: ") + hipGetErrorString((hipError_t)e));
+        int e = 0;
         if (p.use_scratch) {
             HIP_TRY(hipEventRecord(l.finished, c->stream));
             l.used = true;

@@ -461,7 +461,7 @@ class VRendererHIP:
         check(self._lib.vrhip_last_launch_info(self._need_ctx(), ctypes.byref(sp), ctypes.byref(us), ctypes.byref(kd)),
               "vrhip_last_launch_info")
         return {"split": int(sp.value), "use_scratch": int(us.value),
-                "kind": ("render_kernel", "path_pool", "service")[min(int(kd.value), 2)]}
+                "kind": ("render_kernel", "path_pool", "service", "path_pool_graph")[min(int(kd.value), 3)]}
 
     def device_buffers(self):
         a, r, d = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
