@@ -34,7 +34,7 @@ from vrenderer_pathtracer_amd.tiles import WHAT_RGBA8, max_owned_pixels  # noqa:
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C5"
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 F = int(sys.argv[3]) if len(sys.argv) > 3 else 16
-STEPS = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+STEPS = int(sys.argv[4]) if len(sys.argv) > 4 else 100
 XGMI_GBS = float(os.environ.get("XGMI_GBS", "50"))
 GATHER_LAT_US = float(os.environ.get("GATHER_LAT_US", "30"))
 

@@ -112,9 +112,12 @@ def test_service_automatic_mode_and_tiling(native):
 
 
 def test_service_deferred_gather_single_rank(native):
-    """vrhip_comm_gather inside a session (one-rank RCCL communicator): the
-    gathers are deferred to the session's close; the gathered image and the
-    accumulation equal the launch-by-launch render."""
+    """vrhip_comm_gather inside a session (one-rank RCCL communicator,
+    explicit service mode 1): the gathers are deferred to the session's close;
+    the gathered image and the accumulation equal the launch-by-launch render.
+    70 two-frame steps with a gather each: three sessions (32 launch slots
+    each), so the next session's kernel runs while the previous session's
+    deferred gathers are still queued (Session::summed)."""
     from vrenderer_pathtracer_amd.renderer import comm_unique_id
     from vrenderer_pathtracer_amd.tiles import WHAT_ACCUM, WHAT_RGBA8
     sc = scenes.make_scene("C2", 96, 64)
@@ -125,17 +128,19 @@ def test_service_deferred_gather_single_rank(native):
         r.set_service(service)
         r.comm_init(0, 1, comm_unique_id())
         t = sc["time"]
-        for i in range(5):
+        for i in range(70):
             r.render(frames=2, times=[t + 2 * i, t + 2 * i + 1], sync=False)
             r.comm_gather(WHAT_RGBA8)
-            if i == 3:
+            if i % 20 == 3:
                 r.comm_gather(WHAT_ACCUM)
         r.sync()
         out = r.read_accum(), r.read_rgba8(), r.read_depth8()
+        info = r.service_info()
         r.comm_destroy()
         r.cleanUp()
-        return out
-    got, base = run(1), run(0)
+        return out, info
+    (got, gi), (base, _) = run(1), run(0)
+    assert gi["sessions"] >= 3 and gi["deferred_gathers"] >= 70, gi
     for g, b, what in zip(got, base, ("accum", "rgba8", "depth8")):
         _eq(g, b, what)
 

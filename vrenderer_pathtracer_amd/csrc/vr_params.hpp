@@ -219,6 +219,10 @@ int launch_order(uint32_t* cost, uint32_t* order, uint32_t n_sub, uint32_t cap, 
 int launch_half_to_float(const uint16_t* src, vr4* dst, size_t n, void* stream);
 int launch_pack_tiles(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,
                       uint32_t n_owned, uint32_t rank, uint32_t nranks, int unpack, void* stream);
+// the gathering rank: ranks r0..nranks-1's packed buffers (stride_bytes apart,
+// from src) scattered into the image in one launch
+int launch_unpack_ranks(const void* src, void* dst, uint32_t elem_bytes, uint32_t W, uint32_t tiles_x,
+                        uint32_t total_tiles, uint32_t r0, uint32_t nranks, size_t stride_bytes, void* stream);
 int launch_vmem_roof(int width, const uint32_t* tab, uint32_t n_lines, uint32_t distinct, int iters,
                      uint32_t blocks, uint32_t* out, void* stream);
 int launch_selftest_math(int fn, const float* a, const float* b, float* out, size_t n, void* stream);

@@ -197,7 +197,17 @@ struct vrhip_ctx {
         hipEvent_t k0 = nullptr, k1 = nullptr;    // the service kernel's span
         hipEvent_t finished = nullptr;            // recorded on `stream` after the session's finish pass
         bool finished_used = false;
+        // recorded on `stream` right after the finish pass, before the
+        // session's deferred gathers; the next session's kernel waits for it
+        // instead of for everything on `stream` when nothing it reads was
+        // queued there since (stream_epoch unchanged), so it overlaps them
+        hipEvent_t summed = nullptr;
+        uint64_t summed_epoch = 0;
+        bool summed_valid = false;
     } svc;
+    // bumped by everything that queues work the render kernels read on
+    // `stream` (uploads and other quiesce() callers, clears): Session::summed
+    uint64_t stream_epoch = 0;
     int service = -1;                             // 1 every production mesh launch, 0 never, -1 automatic
     // vrhip_set_service_timing (test hook; 0 = default): the kernel's idle
     // limit, the host's post window, a host delay between the window check
@@ -258,6 +268,7 @@ int clear_accum(vrhip_ctx* c)
 {
     int rc = svc_close(c);                        // the open session's results come first
     if (rc != VRHIP_OK) return rc;
+    ++c->stream_epoch;
     c->frame = 1;
     HIP_TRY(hipMemsetAsync(c->accum, 0, sizeof(vr4) * (size_t)c->W * c->H, c->stream));
     return VRHIP_OK;
@@ -527,6 +538,7 @@ bool to_device_layout(const float* bvh, size_t n_bvh_f4, const vr4* verts, const
 void quiesce(vrhip_ctx* c)
 {
     (void)svc_close(c);
+    ++c->stream_epoch;
     if (c->svc.s) (void)hipStreamSynchronize(c->svc.s);
     for (auto& l : c->lane)
         if (l.s) (void)hipStreamSynchronize(l.s);
@@ -1100,8 +1112,10 @@ static void svc_free(vrhip_ctx* c)
     if (S.k0) (void)hipEventDestroy(S.k0);
     if (S.k1) (void)hipEventDestroy(S.k1);
     if (S.finished) (void)hipEventDestroy(S.finished);
+    if (S.summed) (void)hipEventDestroy(S.summed);
     if (S.s) (void)hipStreamDestroy(S.s);
-    S.k0 = S.k1 = S.finished = nullptr;
+    S.k0 = S.k1 = S.finished = S.summed = nullptr;
+    S.summed_valid = false;
     S.s = nullptr;
     S.open = false;
 }
@@ -1182,6 +1196,11 @@ static int svc_close(vrhip_ctx* c)
         const int e = vr::launch_service_finish(S.p, S.fin, S.n_tiles, c->stream);
         if (e != 0) return fail(VRHIP_ERR_HIP, std::string("service finish launch: ") + hipGetErrorString((hipError_t)e));
     }
+    if (!S.gathers.empty()) {
+        HIP_TRY(hipEventRecord(S.summed, c->stream));
+        S.summed_epoch = c->stream_epoch;
+        S.summed_valid = true;
+    }
     // deferred gathers, in call order; rank 0 keeps its own tiles from the
     // finish pass (the final state) and unpacks the other ranks' of every gather
     for (const auto& g : S.gathers) {
@@ -1192,14 +1211,11 @@ static int svc_close(vrhip_ctx* c)
         const size_t bytes = (size_t)S.fin.stage_pixels * esz;
         const ncclResult_t r = ncclGather(send, c->comm_recv, bytes, ncclUint8, 0, c->comm, c->stream);
         if (r != ncclSuccess) return fail(VRHIP_ERR_COMM, std::string("ncclGather: ") + ncclGetErrorString(r));
-        if (c->rank == 0) {
+        if (c->rank == 0 && c->nranks > 1) {
             void* dst = what == 1 ? (void*)c->accum : what == 2 ? (void*)c->depth : (void*)c->rgba;
-            for (uint32_t rr = 1; rr < c->nranks; ++rr) {
-                const uint32_t n_owned = owned_tiles_of(c->W, c->H, rr, c->nranks);
-                const int ee = vr::launch_pack_tiles(c->comm_recv + (size_t)rr * bytes, dst, (uint32_t)esz, c->W,
-                                                     c->W / 16u, n_owned, rr, c->nranks, 1, c->stream);
-                if (ee) return fail(VRHIP_ERR_HIP, "unpack launch failed");
-            }
+            const int ee = vr::launch_unpack_ranks(c->comm_recv + bytes, dst, (uint32_t)esz, c->W, c->W / 16u,
+                                                   (c->W / 16u) * (c->H / 16u), 1u, c->nranks, bytes, c->stream);
+            if (ee) return fail(VRHIP_ERR_HIP, "unpack launch failed");
         }
     }
     S.gathers.clear();
@@ -1224,6 +1240,7 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     if (!S.s) {
         HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&S.finished, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&S.summed, hipEventDisableTiming));
         for (int i = 0; i < 2; ++i) {
             HIP_TRY(hipHostMalloc((void**)&S.rings[i], sizeof(vr::SvcHostCtl), hipHostMallocCoherent | hipHostMallocMapped));
             HIP_TRY(hipHostGetDevicePointer((void**)&S.rings_dev[i], S.rings[i], 0));
@@ -1301,9 +1318,18 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     // the ring: nothing posted, open, the kernel serving (the kernel launch
     // below orders these host stores before the kernel's first read)
     S.host->posted = 0; S.host->closed = 0; S.host->retired = 0;
-    // everything queued on `stream` first (uploads, clears, earlier finish passes)
-    HIP_TRY(hipEventRecord(c->ev_join, c->stream));
-    HIP_TRY(hipStreamWaitEvent(S.s, c->ev_join, 0));
+    // everything queued on `stream` first (uploads, clears, earlier finish
+    // passes) -- or, when the last thing queued there that this session's
+    // kernels depend on is the previous session's finish pass (its scratch,
+    // primary records and pixel list are reused here), only that: its
+    // deferred gathers then run beside this session (Session::summed)
+    if (S.summed_valid && S.summed_epoch == c->stream_epoch) {
+        HIP_TRY(hipStreamWaitEvent(S.s, S.summed, 0));
+    } else {
+        HIP_TRY(hipEventRecord(c->ev_join, c->stream));
+        HIP_TRY(hipStreamWaitEvent(S.s, c->ev_join, 0));
+    }
+    S.summed_valid = false;
     HIP_TRY(hipMemsetAsync(S.dev, 0, sizeof(vr::SvcDevCtl), S.s));
     HIP_TRY(hipMemsetAsync(S.qctl, 0, (size_t)slots * vr::kSvcQctlWords * 4u, S.s));
     HIP_TRY(hipEventRecord(S.k0, S.s));
@@ -2015,13 +2041,20 @@ int vrhip_unpack_tiles(vrhip_ctx* c, int what, const void* src, uint32_t n_ranks
     if (!c || !src || what < 0 || what > 2 || n_ranks == 0) return fail(VRHIP_ERR_INVALID, "bad unpack arguments");
     int rc = set_device(c); if (rc) return rc;
     if ((rc = svc_close(c)) != VRHIP_OK) return rc;
-    const char* s = (const char*)src;
+    if (stride_bytes) {                   // one launch for every rank's buffer
+        const int e = vr::launch_unpack_ranks(src, const_cast<void*>(buf_of(c, what)), (uint32_t)elem_size(what), c->W,
+                                              c->W / 16u, (c->W / 16u) * (c->H / 16u), 0u, n_ranks, stride_bytes,
+                                              c->stream);
+        if (e) return fail(VRHIP_ERR_HIP, "unpack launch failed");
+        return VRHIP_OK;
+    }
+    const char* s = (const char*)src;      // tightly packed: buffers of different lengths, one launch each
     for (uint32_t r = 0; r < n_ranks; ++r) {
         const uint32_t n_owned = owned_tiles_of(c->W, c->H, r, n_ranks);
         int e = vr::launch_pack_tiles(s, const_cast<void*>(buf_of(c, what)), (uint32_t)elem_size(what), c->W,
                                       c->W / 16u, n_owned, r, n_ranks, 1, c->stream);
         if (e) return fail(VRHIP_ERR_HIP, "unpack launch failed");
-        s += stride_bytes ? stride_bytes : (size_t)n_owned * 256u * elem_size(what);
+        s += (size_t)n_owned * 256u * elem_size(what);
     }
     return VRHIP_OK;
 }
@@ -2293,12 +2326,9 @@ static int multi_gather(vrhip_ctx* c, int what)
     if (r != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
     if ((rc = set_device(c)) != VRHIP_OK) return rc;
     const uint32_t n = (uint32_t)c->group.size();
-    for (uint32_t rr = 1; rr < n; ++rr) {               // the lead's own tiles are in place
-        const uint32_t n_owned = owned_tiles_of(c->W, c->H, rr, n);
-        if (vr::launch_pack_tiles(c->comm_recv + (size_t)rr * bytes, const_cast<void*>(buf_of(c, what)), (uint32_t)esz,
-                                  c->W, c->W / 16u, n_owned, rr, n, 1, c->stream) != 0)
-            return fail(VRHIP_ERR_HIP, "unpack launch failed");
-    }
+    if (n > 1 && vr::launch_unpack_ranks(c->comm_recv + bytes, const_cast<void*>(buf_of(c, what)), (uint32_t)esz,
+                                         c->W, c->W / 16u, (c->W / 16u) * (c->H / 16u), 1u, n, bytes, c->stream) != 0)
+        return fail(VRHIP_ERR_HIP, "unpack launch failed");       // (the lead's own tiles are in place)
     return VRHIP_OK;
 }
 
