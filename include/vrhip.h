@@ -236,7 +236,7 @@ int vrhip_set_overlap(vrhip_ctx *ctx, int mode);
  * last, longest paths) overlaps the next launch's paths instead of ending a
  * kernel.  The images are summed, in path order, by one finish pass when the
  * session closes: at the next call on the context that is not vrhip_render or
- * vrhip_comm_gather (sync, read-back, upload, any setting, ...), when its 32
+ * vrhip_comm_gather (sync, read-back, upload, any setting, ...), when its 128
  * launch slots are used, or when a launch does not fit it (another scene,
  * camera or tiling, more frames than its slots hold).  vrhip_comm_gather
  * inside a session gathers the image as of that call when the session closes.

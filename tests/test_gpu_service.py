@@ -66,12 +66,12 @@ def test_service_session_equals_launch_by_launch_and_oracle(native, oracle, cfg,
 
 
 def test_service_session_limits(native, oracle):
-    """Sessions close and reopen on their own: 40 one-frame calls (more than
-    the 32 launch slots), a call of more frames than the session's slots hold
+    """Sessions close and reopen on their own: 140 one-frame calls (more than
+    the 128 launch slots), a call of more frames than the session's slots hold
     (4 after 1-frame launches), a 70-frame call (two launches of 64 + 6).
     Bit-identical to launch-by-launch rendering."""
     sc = scenes.make_scene("C3", 64, 48)
-    calls = [1] * 40 + [4, 1, 70, 2]
+    calls = [1] * 140 + [4, 1, 70, 2]
     (a1, r1, _, n1), _ = _run(sc, calls, 1)
     (a0, r0, _, n0), _ = _run(sc, calls, 0)
     assert n1 == n0 == sum(calls)
@@ -115,7 +115,7 @@ def test_service_deferred_gather_single_rank(native):
     """vrhip_comm_gather inside a session (one-rank RCCL communicator,
     explicit service mode 1): the gathers are deferred to the session's close;
     the gathered image and the accumulation equal the launch-by-launch render.
-    70 two-frame steps with a gather each: three sessions (32 launch slots
+    280 two-frame steps with a gather each: three sessions (128 launch slots
     each), so the next session's kernel runs while the previous session's
     deferred gathers are still queued (Session::summed)."""
     from vrenderer_pathtracer_amd.renderer import comm_unique_id
@@ -128,10 +128,10 @@ def test_service_deferred_gather_single_rank(native):
         r.set_service(service)
         r.comm_init(0, 1, comm_unique_id())
         t = sc["time"]
-        for i in range(70):
+        for i in range(280):
             r.render(frames=2, times=[t + 2 * i, t + 2 * i + 1], sync=False)
             r.comm_gather(WHAT_RGBA8)
-            if i % 20 == 3:
+            if i % 50 == 3:
                 r.comm_gather(WHAT_ACCUM)
         r.sync()
         out = r.read_accum(), r.read_rgba8(), r.read_depth8()
@@ -140,7 +140,7 @@ def test_service_deferred_gather_single_rank(native):
         r.cleanUp()
         return out, info
     (got, gi), (base, _) = run(1), run(0)
-    assert gi["sessions"] >= 3 and gi["deferred_gathers"] >= 70, gi
+    assert gi["sessions"] >= 3 and gi["deferred_gathers"] >= 280, gi
     for g, b, what in zip(got, base, ("accum", "rgba8", "depth8")):
         _eq(g, b, what)
 

@@ -91,7 +91,13 @@ constexpr uint32_t kQueueStride = 256;
 // appends launch descriptors to a ring in host-pinned memory and bumps
 // `posted`; a polling wave mirrors them into device memory; every wave takes
 // chunks of launch L, then L + 1, ... so the launches' drains overlap.
-constexpr uint32_t kSvcMaxLaunches = 32;          // launch slots per session
+// launch slots per session: a session's drain, finish pass and primary pass
+// are paid once per this many launches (r06: 32 -> 128, the 8-way C3 shard
+// steps of a 100-step run 0.229 -> see DESIGN 6)
+#ifndef VR_SVC_SLOTS
+#define VR_SVC_SLOTS 128
+#endif
+constexpr uint32_t kSvcMaxLaunches = VR_SVC_SLOTS;
 struct SvcLaunch {                                 // one launch of a session (272 B)
     uint32_t first_frame, n_frames, pad0, pad1;
     uint32_t times[kMaxFramesPerLaunch];
