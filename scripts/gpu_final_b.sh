@@ -3,7 +3,7 @@
 # FETCH_SIZE / WRITE_SIZE passes of the same bench command.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; TAG=${1:-final}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
-PB="bench.py --steps 5 --warmup 1 --no-cpu --no-roof --interactive-frames 0 --strong-steps 0"
+PB="bench.py --steps 5 --warmup 1 --no-cpu --no-roof --no-verify --interactive-frames 0 --strong-steps 0"
 for cfg in ${CFGS:-C1 C2 C3 C4 C5}; do
   for kind in trace fetch write; do
     case $kind in

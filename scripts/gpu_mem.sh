@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-mem}; CFG=${2:-C2}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
-BENCH="bench.py --steps 3 --warmup 1 --no-cpu --no-roof --interactive-frames 0 --config $CFG"
+BENCH="bench.py --steps 3 --warmup 1 --no-cpu --no-roof --no-verify --interactive-frames 0 --config $CFG"
 i=0
 for PMC in "GRBM_GUI_ACTIVE TA_TA_BUSY_sum" "TD_TD_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" \
            "TD_TC_STALL_sum TCP_PENDING_STALL_CYCLES_sum" "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum" \

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-valu}; CFG=${2:-C2}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
-BENCH="bench.py --steps 3 --warmup 1 --no-cpu --no-roof --interactive-frames 0 --strong-steps 0 --config $CFG"
+BENCH="bench.py --steps 3 --warmup 1 --no-cpu --no-roof --no-verify --interactive-frames 0 --strong-steps 0 --config $CFG"
 i=0
 for PMC in "GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32" \
            "SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64 SQ_INST_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD" \
