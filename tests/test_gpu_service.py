@@ -389,3 +389,42 @@ def test_one_frame_graph_equals_launches(native, oracle, cfg):
     oa, _, _, _ = po.render(sc, frames=6, times=[sc["time"] + k for k in range(6)], libm=po.LIBM_PORTABLE)
     H, W = (64 // 16) * 16, (96 // 16) * 16
     _eq(g[0][:H, :W], oa[:H, :W], "graph accum@6 vs oracle")
+
+
+def test_service_scratch_shortage_takes_the_launch_path(native):
+    """A session whose launch slots do not fit in half of the device memory
+    free when it opens is not opened: its launches take the launch path
+    (vrhip_service_info counts the fallback) and the image equals
+    launch-by-launch rendering.  Forced by holding all but ~1.2 GB of the
+    device memory in a torch tensor after a first (launch-path) call has
+    allocated its scratch; two 376-MB C3 slots then exceed the half.
+    (Automatic mode: the first two calls of the burst take the launch path,
+    the later ones would open a session.)"""
+    import torch
+    sc = scenes.make_scene("C3")
+
+    def run(service, hog):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_service(service)
+        r.set_service_budget(1 << 40)          # the budget allows the slots: the free-memory cap decides
+        t = sc["time"]
+        r.render(frames=16, times=[t + k for k in range(16)], sync=True)
+        hold = None
+        if hog:
+            free, _ = torch.cuda.mem_get_info(0)
+            hold = torch.empty(max(0, free - (1200 << 20)), dtype=torch.uint8, device="cuda:0")
+        kinds = []
+        for i in range(1, 4):
+            r.render(frames=16, times=[t + 16 * i + k for k in range(16)], sync=False)
+            kinds.append(r.last_launch_info()["kind"])
+        out = r.read_accum(), r.read_rgba8()
+        info = r.service_info()
+        r.cleanUp()
+        del hold
+        torch.cuda.empty_cache()
+        return out, kinds, info
+    (a1, r1), k1, i1 = run(-1, True)       # automatic: calls 3-4 are behind a launch in flight
+    (a0, r0), _, _ = run(0, False)
+    assert i1["alloc_fallbacks"] >= 1 and "service" not in k1, (i1, k1)
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8")
