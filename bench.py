@@ -117,7 +117,8 @@ def executed_loads(e: dict) -> dict:
     visits not served from LDS (2x16 B per conservative fp16 node), triangle
     pairs (4x16 + 8 B), primary records (2x16 B per path), hit attributes
     (uv 3x8, tangents / normals 3x16, face-normal vertices 3x12 -- those the
-    scene's specialised kernel loads), texels and HDRI (16 B), BRDF entries (4 B)."""
+    scene's specialised kernel loads), texels and HDRI (16 B), BRDF entries (12 B: the device table is
+    interleaved RGB, round 6)."""
     return {16: e["lane_loads_b128"], 12: e["lane_loads_b96"], 8: e["lane_loads_b64"], 4: e["lane_loads_b32"]}
 
 

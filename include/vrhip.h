@@ -134,7 +134,8 @@ int vrhip_upload_hdr_half(vrhip_ctx *ctx, const uint16_t *rgba_half, uint32_t w,
 int vrhip_upload_texture(vrhip_ctx *ctx, int type, const float *rgba, uint32_t w, uint32_t h);
 /* replaces the device half of vRendererCuda::loadBRDF
  * (src/vRendererCuda.cpp:413-437) + cu_bindBRDF: float[3*90*90*180] planar
- * R,G,B MERL table.  Copies; does NOT take ownership (the C++ adapter
+ * R,G,B MERL table.  Copies (interleaving the channels on the device, so a
+ * lookup reads one cache line); does NOT take ownership (the C++ adapter
  * reproduces the reference's delete[]). */
 int vrhip_upload_brdf(vrhip_ctx *ctx, const float *table, size_t n_floats);
 

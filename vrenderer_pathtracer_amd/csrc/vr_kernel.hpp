@@ -893,9 +893,10 @@ __device__ __forceinline__ vr4 lookup_brdf(const float* __restrict__ T, vr4 refl
     }
     const int ind = phi_diff_index(phi_diff) + theta_diff_index(theta_diff) * 360 / 2
                     + theta_half_index(theta_H) * 360 / 2 * 90;
-    return mk4((float)((double)T[ind] * (1.0 / 1500.0)),
-               (float)((double)T[ind + 1458000] * (1.15 / 1500.0)),
-               (float)((double)T[ind + 2916000] * (1.66 / 1500.0)), 0.f);
+    const float* e = T + 3 * ind;    // interleaved on the device (vrhip_upload_brdf)
+    return mk4((float)((double)e[0] * (1.0 / 1500.0)),
+               (float)((double)e[1] * (1.15 / 1500.0)),
+               (float)((double)e[2] * (1.66 / 1500.0)), 0.f);
 }
 
 // thrust::minstd_rand + uniform_real_distribution<float>(0,1) (rocThrust
@@ -1155,7 +1156,7 @@ __device__ __forceinline__ bool bounce_step(const RenderParams& p, Ray& ray, con
                                            mul4s(w, sqrt_exact(1 - rand2))));
         if HAS(F_BRDF) {
             const float dw = 24 * pow_p(newdir.x * newdir.x + newdir.y * newdir.y + newdir.z * newdir.z, -1.5f);
-            if (COUNT) { cnt.brdf++; cnt.ld32 += 3; }
+            if (COUNT) { cnt.brdf++; cnt.ld96 += 1; }
             const vr4 b = lookup_brdf(p.brdf, newdir, ray.d, h.n, h.tan);
             const vr4 bm = mk4(__builtin_fmaxf(b.x, 0.f), __builtin_fmaxf(b.y, 0.f), __builtin_fmaxf(b.z, 0.f),
                                __builtin_fmaxf(b.w, 0.f));
