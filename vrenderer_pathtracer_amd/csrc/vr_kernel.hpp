@@ -325,6 +325,9 @@ __device__ __forceinline__ int trav_pop(Trav& tr, const Lds& L)
 #ifndef VR_SVC_LDS_NODES
 #define VR_SVC_LDS_NODES 1
 #endif
+#ifndef VR_LDS_PER_LANE
+#define VR_LDS_PER_LANE 0
+#endif
 template <uint32_t FEAT>
 constexpr bool lds_nodes_on() {
     return VR_SVC_LDS_NODES != 0 || (FEAT & F_SERVICE) == 0u || (FEAT & F_CORNELL) == 0u;
@@ -345,8 +348,9 @@ __device__ __forceinline__ void node_step(const RenderParams& p, const Ray& r, T
     int idx0, idx1;
     const int node = tr.nodeAddr >> 2;
     // wave-uniform choice between the LDS copy and L2/HBM: a diverged wave
-    // would pay both round trips
-    const bool in_lds = lds_nodes_on<FEAT>() && __ballot(node >= L.n_cached) == 0ull;
+    // would pay both round trips (VR_LDS_PER_LANE=1: each lane on its own)
+    const bool in_lds = lds_nodes_on<FEAT>() &&
+                        (VR_LDS_PER_LANE ? node < L.n_cached : __ballot(node >= L.n_cached) == 0ull);
     if (COUNT) {
         cnt.nodes_lds += in_lds ? 1u : 0u;
         if (!in_lds) { cnt.ld128 += strict ? 3u : 2u; cnt.ld64 += strict ? 1u : 0u; }
