@@ -1769,12 +1769,17 @@ constexpr int path_cache_nodes(int stack, int bt, bool c) {
 #ifndef VR_SVC_CORNELL_RES
 #define VR_SVC_CORNELL_RES 1
 #endif
+#ifndef VR_ONEFRAME_CORNELL_RES
+#define VR_ONEFRAME_CORNELL_RES 0    // 1: one-frame Cornell kernels at the 7-wave residency (A/B builds)
+#endif
 template <uint32_t FEAT>
 constexpr bool cornell_kernel() {
     // the one-frame kernels (F_INLINE_PRIM) keep 6 waves: at 7 the interactive
     // C2 rate fell 2,147 -> 2,100 Mpaths/s (r02g); so do the small-launch
     // kernels (F_SMALL), which spilled 19 VGPRs at 7 with helper lanes and
     // cost counting (8-rank C2 shard step 1.317 -> 1.257 ms at 6, r03p)
+    if (VR_ONEFRAME_CORNELL_RES && (FEAT & F_EXACT) != 0u && (FEAT & F_CORNELL) != 0u && (FEAT & F_INLINE_PRIM) != 0u)
+        return true;
     return (FEAT & F_EXACT) != 0u && (FEAT & F_CORNELL) != 0u && (FEAT & F_INLINE_PRIM) == 0u &&
            (FEAT & (F_SMALL | (VR_SVC_CORNELL_RES ? 0u : (uint32_t)F_SERVICE))) == 0u;
 }
