@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define VRHIP_ABI_VERSION 4
+#define VRHIP_ABI_VERSION 5
 
 typedef enum vrhip_status {
     VRHIP_OK = 0,
@@ -55,7 +55,8 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx **out);
 /* One renderer over several GPUs of this process (SURVEY 8(b) "create_multi";
  * no reference counterpart: the reference's caller creates one renderer,
  * src/NGLScene.cpp:82-89).  A member context per device in `devices` (no
- * repeats), each rendering the 16x16 tiles i, i + n, ... of the image; the
+ * repeats), member i rendering the 16x16 tiles vrhip_set_tiling deals rank i
+ * of n; the
  * RCCL communicators are made in one call (ncclCommInitAll).  The returned
  * context is the lead (devices[0]): every setting and upload on it fans out
  * to all members; vrhip_render renders every device's tiles (each member
@@ -310,9 +311,13 @@ int vrhip_read_depth8(vrhip_ctx *ctx, uint8_t *out_rgba8);       /* uchar4[W*H] 
 int vrhip_device_buffers(vrhip_ctx *ctx, void **accum, void **rgba8, void **depth8);
 
 /* ---- multi-GPU image-tile sharding ------------------------------------ */
-/* Render only the 16x16 tiles t (row-major over the rendered region) with
- * t % n_ranks == rank: tiles dealt round-robin, so every rank gets the same
- * number of tiles (+-1) spread over the whole image (sky vs mesh balance).
+/* Render only the 16x16 tiles dealt to `rank`: rank r holds the tiles at
+ * positions s = r, r + n_ranks, r + 2 n_ranks, ... of the dealing sequence,
+ * and position s is the tile in row s / tiles_x, column
+ * (s % tiles_x + s / tiles_x) % tiles_x (tiles_x = width / 16; each row
+ * rotated by its index, ABI 5 -- ABI 4 dealt row-major, which gives every
+ * rank fixed columns when tiles_x is a multiple of n_ranks).  Every rank gets
+ * the same number of tiles (+-1) spread over the whole image.
  * Seeds use global pixel coordinates, so the union of the ranks' tiles equals
  * the 1-GPU image bit for bit.  VRHIP_ERR_INVALID while a communicator
  * (vrhip_comm_init) with another tiling exists. */

@@ -1358,8 +1358,8 @@ __global__ void __launch_bounds__(kBlockThreads, render_waves<FEAT>(STACK)) rend
     const uint32_t g = blockIdx.x - tile * T;
     const int wave = tid >> 6, lane = tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
-    const uint32_t tile_y = gtile / p.tiles_x;
-    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t tile_y = tile_row(gtile, p.tiles_x);
+    const uint32_t tile_x = tile_col(gtile, p.tiles_x);
     const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
     const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     if (x >= p.wr || y >= p.hr) return;   // never true for a valid launch
@@ -1496,8 +1496,8 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
     const uint32_t tile = blockIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
-    const uint32_t tile_y = gtile / p.tiles_x;
-    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t tile_y = tile_row(gtile, p.tiles_x);
+    const uint32_t tile_x = tile_col(gtile, p.tiles_x);
     const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
     const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;
@@ -1797,8 +1797,8 @@ __device__ __forceinline__ void sub_pixel(const RenderParams& p, uint32_t sub, u
 {
     const uint32_t tile = sub >> 2, quad = sub & 3u;
     const uint32_t gtile = p.rank + tile * p.nranks;       // tiles dealt round-robin to ranks
-    const uint32_t tile_y = gtile / p.tiles_x;
-    const uint32_t tile_x = gtile - tile_y * p.tiles_x;
+    const uint32_t tile_y = tile_row(gtile, p.tiles_x);
+    const uint32_t tile_x = tile_col(gtile, p.tiles_x);
     x = tile_x * 16u + (quad & 1u) * 8u + (px & 7u);
     y = tile_y * 16u + (quad >> 1) * 8u + (px >> 3);
 }

@@ -4,6 +4,22 @@
 #include <stddef.h>
 #include <stdint.h>
 
+// The tile at index gt of the dealing sequence (rank r holds r, r+N, r+2N, ...):
+// row gt / tiles_x, column (gt mod tiles_x + row) mod tiles_x.  Rotating each
+// row by its index deals a rank diagonals: with plain row-major dealing and a
+// tile row a multiple of N (every BASELINE size at N = 2, 4, 8) a rank held
+// fixed tile columns, and the columns' costs differ -- 8-rank rehearsal, the
+// slowest rank's step C2 0.799 -> 0.786 ms, C3 0.218 -> 0.210 ms
+// (profiles/r06z).  VR_TILE_STAGGER=0: row-major dealing (A/B builds).
+#ifndef VR_TILE_STAGGER
+#define VR_TILE_STAGGER 1
+#endif
+constexpr uint32_t tile_row(uint32_t gt, uint32_t tiles_x) { return gt / tiles_x; }
+constexpr uint32_t tile_col(uint32_t gt, uint32_t tiles_x)
+{
+    return VR_TILE_STAGGER ? (gt % tiles_x + gt / tiles_x) % tiles_x : gt % tiles_x;
+}
+
 namespace vr {
 
 // float4 / float2 with the reference's memory layout (16 B / 8 B aligned)

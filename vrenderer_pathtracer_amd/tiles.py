@@ -4,8 +4,9 @@ The reference is single-GPU; its RNG seeds depend only on global pixel
 coordinates, frame and time (cuda/src/PathTracer.cu:817-818), so any
 partition of the pixels renders the same image bit for bit.  Partition:
 16x16 tiles (the reference's block, PathTracer.cu:887) dealt round-robin to
-ranks in row-major tile order, so ranks own equal tile counts (+-1) spread
-over the whole image (sky vs mesh load balance).  Each rank keeps its own
+ranks along a row-rotated tile order (row y's tiles start at column y mod
+tiles_x; include/vrhip.h vrhip_set_tiling), so ranks own equal tile counts
+(+-1) in diagonals spread over the whole image (sky vs mesh load balance).  Each rank keeps its own
 float4 accumulation resident; after every accumulation step the ranks' RGBA8
 tiles (or float4 accumulation, for parity read-out) are gathered to rank 0
 with ONE collective (ncclGather over xGMI inside libvrhip.so,
