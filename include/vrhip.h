@@ -316,7 +316,8 @@ int vrhip_device_buffers(vrhip_ctx *ctx, void **accum, void **rgba8, void **dept
  * and position s is the tile in row s / tiles_x, column
  * (s % tiles_x + s / tiles_x) % tiles_x (tiles_x = width / 16; each row
  * rotated by its index, ABI 5 -- ABI 4 dealt row-major, which gives every
- * rank fixed columns when tiles_x is a multiple of n_ranks).  Every rank gets
+ * rank fixed columns when tiles_x is a multiple of n_ranks); with
+ * n_ranks == 1 the order stays row-major.  Every rank gets
  * the same number of tiles (+-1) spread over the whole image.
  * Seeds use global pixel coordinates, so the union of the ranks' tiles equals
  * the 1-GPU image bit for bit.  VRHIP_ERR_INVALID while a communicator

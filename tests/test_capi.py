@@ -244,7 +244,7 @@ def test_tile_pixels_partition(native, W, H, n):
     for r, pix in enumerate(parts):
         y, x = pix // W, pix % W
         ty, tx = (y // 16).astype(np.int64), (x // 16).astype(np.int64)
-        s = ty * tiles_x + (tx - ty) % tiles_x                # the tile's position in the dealing sequence
+        s = ty * tiles_x + ((tx - ty) % tiles_x if n > 1 else tx)   # the tile's position in the dealing sequence
         assert (s % n == r).all()
     sizes = [len(p) // 256 for p in parts]
     assert max(sizes) - min(sizes) <= 1

@@ -20,7 +20,7 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
     const int wave = (int)tid >> 6, lane = (int)tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
     const uint32_t tile_y = tile_row(gtile, p.tiles_x);
-    const uint32_t tile_x = tile_col(gtile, p.tiles_x);
+    const uint32_t tile_x = tile_col(gtile, p.tiles_x, p.nranks);
     const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
     const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     if (x >= p.wr || y >= p.hr) return;
@@ -129,7 +129,7 @@ __global__ void pack_tiles_kernel(const uint32_t* __restrict__ src, uint32_t* __
 {
     const uint32_t j = blockIdx.x;
     const uint32_t gt = rank + j * nranks;
-    const uint32_t ty = tile_row(gt, tiles_x), tx = tile_col(gt, tiles_x);
+    const uint32_t ty = tile_row(gt, tiles_x), tx = tile_col(gt, tiles_x, nranks);
     for (uint32_t w = threadIdx.x; w < 256u * wpp; w += blockDim.x) {
         const uint32_t px = w / wpp, word = w - px * wpp;
         const size_t full = ((size_t)(ty * 16u + px / 16u) * W + tx * 16u + px % 16u) * wpp + word;
@@ -153,7 +153,7 @@ __global__ void unpack_ranks_kernel(const uint32_t* __restrict__ src, uint32_t* 
     if (j >= n_owned) return;
     const uint32_t* s = src + (size_t)blockIdx.y * stride_words;
     const uint32_t gt = rank + j * nranks;
-    const uint32_t ty = tile_row(gt, tiles_x), tx = tile_col(gt, tiles_x);
+    const uint32_t ty = tile_row(gt, tiles_x), tx = tile_col(gt, tiles_x, nranks);
     for (uint32_t w = threadIdx.x; w < 256u * wpp; w += blockDim.x) {
         const uint32_t px = w / wpp, word = w - px * wpp;
         dst[((size_t)(ty * 16u + px / 16u) * W + tx * 16u + px % 16u) * wpp + word] = s[((size_t)j * 256u + px) * wpp + word];
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(kBlockThreads) svc_finish_kernel(const RenderP
     const int wave = (int)tid >> 6, lane = (int)tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;
     const uint32_t tile_y = tile_row(gtile, p.tiles_x);
-    const uint32_t tile_x = tile_col(gtile, p.tiles_x);
+    const uint32_t tile_x = tile_col(gtile, p.tiles_x, p.nranks);
     const uint32_t lx = (uint32_t)((wave & 1) * 8 + (lane & 7)), ly = (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     const uint32_t x = tile_x * 16u + lx, y = tile_y * 16u + ly;
     if (x >= p.wr || y >= p.hr) return;

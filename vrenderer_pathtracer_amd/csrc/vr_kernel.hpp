@@ -1359,7 +1359,7 @@ __global__ void __launch_bounds__(kBlockThreads, render_waves<FEAT>(STACK)) rend
     const int wave = tid >> 6, lane = tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
     const uint32_t tile_y = tile_row(gtile, p.tiles_x);
-    const uint32_t tile_x = tile_col(gtile, p.tiles_x);
+    const uint32_t tile_x = tile_col(gtile, p.tiles_x, p.nranks);
     const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
     const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     if (x >= p.wr || y >= p.hr) return;   // never true for a valid launch
@@ -1497,7 +1497,7 @@ __global__ void __launch_bounds__(kBlockThreads) primary_kernel(const RenderPara
     const int wave = tid >> 6, lane = tid & 63;
     const uint32_t gtile = p.rank + tile * p.nranks;      // tiles dealt round-robin to ranks
     const uint32_t tile_y = tile_row(gtile, p.tiles_x);
-    const uint32_t tile_x = tile_col(gtile, p.tiles_x);
+    const uint32_t tile_x = tile_col(gtile, p.tiles_x, p.nranks);
     const uint32_t x = tile_x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
     const uint32_t y = tile_y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
     constexpr bool CNT = (FEAT & F_COUNT_EXEC) != 0u;
@@ -1798,7 +1798,7 @@ __device__ __forceinline__ void sub_pixel(const RenderParams& p, uint32_t sub, u
     const uint32_t tile = sub >> 2, quad = sub & 3u;
     const uint32_t gtile = p.rank + tile * p.nranks;       // tiles dealt round-robin to ranks
     const uint32_t tile_y = tile_row(gtile, p.tiles_x);
-    const uint32_t tile_x = tile_col(gtile, p.tiles_x);
+    const uint32_t tile_x = tile_col(gtile, p.tiles_x, p.nranks);
     x = tile_x * 16u + (quad & 1u) * 8u + (px & 7u);
     y = tile_y * 16u + (quad >> 1) * 8u + (px >> 3);
 }

@@ -5,7 +5,8 @@
 #include <stdint.h>
 
 // The tile at index gt of the dealing sequence (rank r holds r, r+N, r+2N, ...):
-// row gt / tiles_x, column (gt mod tiles_x + row) mod tiles_x.  Rotating each
+// row gt / tiles_x, column (gt mod tiles_x + row) mod tiles_x when N > 1
+// (one rank: row-major, the order the one-GPU kernels were tuned on).  Rotating each
 // row by its index deals a rank diagonals: with plain row-major dealing and a
 // tile row a multiple of N (every BASELINE size at N = 2, 4, 8) a rank held
 // fixed tile columns, and the columns' costs differ -- 8-rank rehearsal, the
@@ -15,9 +16,9 @@
 #define VR_TILE_STAGGER 1
 #endif
 constexpr uint32_t tile_row(uint32_t gt, uint32_t tiles_x) { return gt / tiles_x; }
-constexpr uint32_t tile_col(uint32_t gt, uint32_t tiles_x)
+constexpr uint32_t tile_col(uint32_t gt, uint32_t tiles_x, uint32_t nranks)
 {
-    return VR_TILE_STAGGER ? (gt % tiles_x + gt / tiles_x) % tiles_x : gt % tiles_x;
+    return (VR_TILE_STAGGER && nranks > 1u) ? (gt % tiles_x + gt / tiles_x) % tiles_x : gt % tiles_x;
 }
 
 namespace vr {

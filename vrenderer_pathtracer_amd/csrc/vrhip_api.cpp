@@ -2012,7 +2012,7 @@ int vrhip_tile_pixels(uint32_t width, uint32_t height, uint32_t rank, uint32_t n
     *n_pix = n_owned * 256u;
     if (pix_out) {
         for (uint32_t j = 0; j < n_owned; ++j) {
-            const uint32_t gt = rank + j * n_ranks, ty = tile_row(gt, tiles_x), tx = tile_col(gt, tiles_x);
+            const uint32_t gt = rank + j * n_ranks, ty = tile_row(gt, tiles_x), tx = tile_col(gt, tiles_x, n_ranks);
             for (uint32_t px = 0; px < 256u; ++px)
                 pix_out[j * 256u + px] = (ty * 16u + px / 16u) * width + tx * 16u + px % 16u;
         }
