@@ -1266,7 +1266,9 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     size_t slot_bytes = 0;
     uint32_t slots = svc_slots(c, p.path_stride, kmax, &slot_bytes);
     const uint32_t stage_px = owned_tiles_of(c->W, c->H, 0, c->nranks) * 256u;   // rank 0 owns the most tiles
-    const size_t stage_bytes = (24u * (size_t)stage_px + 255u) & ~(size_t)255u;
+    // staged images serve deferred gathers only, which need a communicator
+    // (vrhip_comm_init closes any open session, so none appears mid-session)
+    const size_t stage_bytes = c->comm ? (24u * (size_t)stage_px + 255u) & ~(size_t)255u : 0u;
     // the slots' scratch grows into at most half of the device memory free
     // now (plus what the session already holds): several contexts or ranks
     // on one GPU share it, and the launch path needs its own scratch
@@ -1297,7 +1299,7 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     };
     if ((rc = grow(S.scratch, S.scratch_cap, (size_t)slots * slot_bytes)) != VRHIP_OK) return rc;
     if ((rc = grow(S.prim, S.prim_cap, 32u * stride)) != VRHIP_OK) return rc;
-    if ((rc = grow(S.staging, S.staging_cap, (size_t)slots * stage_bytes)) != VRHIP_OK) return rc;
+    if (stage_bytes && (rc = grow(S.staging, S.staging_cap, (size_t)slots * stage_bytes)) != VRHIP_OK) return rc;
     if ((rc = grow(S.qctl, S.qctl_slots, (size_t)slots * vr::kSvcQctlWords * 4u)) != VRHIP_OK) return rc;
     // HDRI scenes: escaped camera rays' pixels leave the session's paths (F_SPARSE)
     const bool sparse = VR_SPARSE_HDRI != 0 && !c->cornell && (p.flags & vr::F_STRICT) == 0u;
@@ -1318,7 +1320,7 @@ static int svc_open(vrhip_ctx* c, const vr::RenderParams& p, int stack, uint32_t
     S.key = svc_key(p);
     std::memset(&S.fin, 0, sizeof(S.fin));
     S.fin.first_frame = c->frame;
-    S.fin.staging = S.staging; S.fin.stage_bytes = stage_bytes; S.fin.stage_pixels = stage_px;
+    S.fin.staging = stage_bytes ? S.staging : nullptr; S.fin.stage_bytes = stage_bytes; S.fin.stage_pixels = stage_px;
     S.gathers.clear();
     // the ring: nothing posted, open, the kernel serving (the kernel launch
     // below orders these host stores before the kernel's first read)
@@ -2117,7 +2119,7 @@ int vrhip_comm_gather(vrhip_ctx* c, int what)
     if (!c || what < 0 || what > 2) return fail(VRHIP_ERR_INVALID, "bad gather arguments");
     if (!c->comm) return fail(VRHIP_ERR_INVALID, "vrhip_comm_init has not been called");
     int rc = set_device(c); if (rc) return rc;
-    if (c->service > 0 && c->svc.open && c->svc.posted > 0) {
+    if (c->service > 0 && c->svc.open && c->svc.posted > 0 && c->svc.fin.staging) {
         // explicit service mode only: inside a session the image after its
         // last launch is staged by the session's finish pass and gathered
         // when the session closes (the caller syncs before any host-side
