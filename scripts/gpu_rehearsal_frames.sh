@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r06zf; mkdir -p $O
-for spec in C3:16:100 C3:32:50 C3:64:25 C2:16:100 C2:64:25; do
+for spec in ${SPECS:-C3:16:100 C3:32:50 C3:64:25 C2:16:100 C2:64:25}; do
   IFS=: read cfg fr st <<< "$spec"
   timeout -k 10 300 python3 scripts/rank_rehearsal.py $cfg 8 $fr $st > $O/reh_${cfg}_$fr.json 2> $O/reh_${cfg}_$fr.err
   rc=$?; echo "$spec rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/reh_${cfg}_$fr.err; exit $rc; }
