@@ -8,6 +8,13 @@ namespace vr {
 // Split launches: sums each pixel's path results in path order (the same
 // float4 operations, in the same order, as the unsplit kernel), then writes
 // the accumulation, colour and depth.
+// Path results loaded per batch ahead of the finish passes' in-order adds:
+// with one load in flight per thread, a shard's session finish (a few blocks
+// per CU) was latency-bound -- 8-rank rehearsal C2 0.917 -> 0.927, C3 0.686
+// -> 0.715 of linear (profiles/r06zl); whole frames unchanged
+#ifndef VR_SVC_FINISH_BATCH
+#define VR_SVC_FINISH_BATCH 8
+#endif
 __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParams p)
 {
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
@@ -40,10 +47,19 @@ __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParam
         for (uint32_t q = 0; q < n_paths; ++q) io = add4(io, h);
         last_w = 1.f;
     } else {
-        for (uint32_t q = 0; q < n_paths; ++q) {
-            const vr3 r = src[(size_t)q * p.path_stride];
-            last_w = (cornell && escaped(r.x)) ? 0.f : depth;
-            io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
+        // loads batched ahead of the in-order adds, as in svc_finish_kernel
+        for (uint32_t q0 = 0; q0 < n_paths; q0 += VR_SVC_FINISH_BATCH) {
+            vr3 r[VR_SVC_FINISH_BATCH];
+#pragma unroll
+            for (int j = 0; j < VR_SVC_FINISH_BATCH; ++j)
+                if (q0 + j < n_paths) r[j] = src[(size_t)(q0 + j) * p.path_stride];
+#pragma unroll
+            for (int j = 0; j < VR_SVC_FINISH_BATCH; ++j) {
+                if (q0 + j < n_paths) {
+                    last_w = (cornell && escaped(r[j].x)) ? 0.f : depth;
+                    io = add4(io, mul4s(mk4(r[j].x, r[j].y, r[j].z, last_w), 1.f / 2.f));
+                }
+            }
         }
     }
     const unsigned char db = f2u8((1.f - last_w) * 255);
@@ -259,10 +275,21 @@ __global__ void __launch_bounds__(kBlockThreads) svc_finish_kernel(const RenderP
         } else {
             const float depth = reinterpret_cast<const float*>(p.paths + (size_t)2u * p.svc_kmax * p.path_stride)[slot];
             const vr3* src = base + slot;
-            for (uint32_t q = 0; q < n_paths; ++q) {
-                const vr3 r = src[(size_t)q * p.path_stride];
-                last_w = (cornell && escaped(r.x)) ? 0.f : depth;
-                io = add4(io, mul4s(mk4(r.x, r.y, r.z, last_w), 1.f / 2.f));
+            // VR_SVC_FINISH_BATCH results loaded before they are added (in
+            // path order): a shard's session has few blocks per CU, and one
+            // load in flight per thread left its finish pass latency-bound
+            for (uint32_t q0 = 0; q0 < n_paths; q0 += VR_SVC_FINISH_BATCH) {
+                vr3 r[VR_SVC_FINISH_BATCH];
+#pragma unroll
+                for (int j = 0; j < VR_SVC_FINISH_BATCH; ++j)
+                    if (q0 + j < n_paths) r[j] = src[(size_t)(q0 + j) * p.path_stride];
+#pragma unroll
+                for (int j = 0; j < VR_SVC_FINISH_BATCH; ++j) {
+                    if (q0 + j < n_paths) {
+                        last_w = (cornell && escaped(r[j].x)) ? 0.f : depth;
+                        io = add4(io, mul4s(mk4(r[j].x, r[j].y, r[j].z, last_w), 1.f / 2.f));
+                    }
+                }
             }
         }
         frame += f.n_frames[L];
