@@ -69,11 +69,13 @@ class TileGather:
     library's own RCCL communicator -- rank 0 draws the id
     (vrhip_comm_unique_id), torch.distributed only hands it to the other
     ranks, and every step is vrhip_comm_gather (pack, ncclGather, unpack on
-    rank 0, enqueued on the renderer's stream -- or, while the renderer's
-    render-service session is open, deferred to the session's close, i.e. to
-    the next call that is not a render: call renderer.sync() before any
-    host-side barrier with the other ranks, as bench.py does, or a rank whose
-    gather is still deferred never joins the collective).  backend "gloo" (a CPU/one-GPU
+    rank 0, enqueued on the renderer's stream -- or, in explicit service mode
+    (renderer.set_service(1)) while a render-service session is open,
+    deferred to the session's close, i.e. to the next call that closes it
+    (include/vrhip.h lists them): call renderer.sync() before any host-side
+    barrier with the other ranks, as bench.py does, or a rank whose gather is
+    still deferred never joins the collective; the automatic mode never
+    defers).  backend "gloo" (a CPU/one-GPU
     rehearsal of the multi-rank path with several ranks sharing a device,
     which RCCL refuses): packed buffers staged through host memory and
     gathered by torch.distributed.
