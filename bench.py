@@ -266,8 +266,11 @@ def main():
     ap.add_argument("--strong", action="store_true", help="(the default) 16 frames per step for any N")
     ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--interactive-frames", type=int, default=30,
+    ap.add_argument("--interactive-frames", type=int, default=60,
                     help="frames of the one-frame-per-call measurement (0: skip)")
+    ap.add_argument("--interactive-warmup", type=int, default=30,
+                    help="untimed one-frame calls before it (the first ~20 ms of calls after a clear run "
+                         "2-3 %% slower: profiles/r06zt/README.md)")
     ap.add_argument("--strong-steps", type=int, default=20,
                     help="steps of the secondary measurement (N > 1: the 16 x N-frame steps under 'samples_weak', "
                          "and the one-GPU 16-frame reference of 'strong'; 0: skip)")
@@ -484,7 +487,8 @@ def main():
         r.set_kernel_timing(False)
         r.set_service(-1)
         base = scene["time"] + 100000
-        for i in range(3):
+        nw = max(1, args.interactive_warmup)
+        for i in range(nw):
             r.render(frames=1, times=[base + i], sync=True)
             gather.step()
         r.sync()
@@ -494,7 +498,7 @@ def main():
         for i in range(args.interactive_frames):
             # one synchronisation per frame, as vRendererCuda::render's
             # cudaStreamSynchronize (the tile gather, N > 1, is inside it)
-            r.render(frames=1, times=[base + 3 + i], sync=False)
+            r.render(frames=1, times=[base + nw + i], sync=False)
             gather.step()
             r.sync()
         if world > 1:
@@ -505,7 +509,7 @@ def main():
         te = float(te.item())
         r.set_kernel_timing(True)
         pf = (W // 16) * 16 * (H // 16) * 16 * 2
-        inter = {"frames_per_step": 1, "frames": args.interactive_frames,
+        inter = {"frames_per_step": 1, "frames": args.interactive_frames, "warmup_frames": nw,
                  "value": round(pf * args.interactive_frames / te / 1e6, 3), "unit": "Mpaths/s",
                  "ms_per_frame": round(te / args.interactive_frames * 1e3, 4),
                  "note": "one frame per synchronous render() call (src/vRendererCuda.cpp:107-165 syncs every "

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define VRHIP_ABI_VERSION 5
+#define VRHIP_ABI_VERSION 6
 
 typedef enum vrhip_status {
     VRHIP_OK = 0,
@@ -212,7 +212,26 @@ int vrhip_render_counted(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *time
 #define VRHIP_PROFILE_COUNTERS 17
 int vrhip_render_profiled(vrhip_ctx *ctx, uint32_t n_frames, const uint32_t *times, uint32_t time_seed,
                           uint64_t counters[VRHIP_PROFILE_COUNTERS]);
+/* Waits until every render queued on the context is complete: the
+ * accumulation, colour and depth images hold it (cudaStreamSynchronize in
+ * vRendererCuda::render, src/vRendererCuda.cpp:107-165).  After a call of one
+ * launch on the context stream (one frame per call, the reference's cadence)
+ * it returns as soon as the finish pass's last block has stored its results:
+ * the pass counts its blocks' arrivals and the last one stores the call's
+ * number to host-coherent memory, which vrhip_sync polls -- about 8 us
+ * before the stream's own completion signal reaches the host.  Work the
+ * library or the caller queues on the context stream afterwards is ordered
+ * behind the pass as usual.  A context whose stream or buffers were handed
+ * out (vrhip_get_stream, vrhip_set_stream, vrhip_device_buffers: the caller
+ * may read the images from its own streams) always waits for the stream, as
+ * does a context with a communicator.  vrhip_set_sync_flag(ctx, 0), or
+ * VRHIP_SYNC_FLAG=0 in the environment at creation, turns the flag off. */
 int vrhip_sync(vrhip_ctx *ctx);
+int vrhip_set_sync_flag(vrhip_ctx *ctx, int on);
+/* Synchronisations since the context was created (diagnostics): out[0] ended
+ * by the completion flag, out[1] by waiting for the stream. */
+#define VRHIP_SYNC_INFO 2
+int vrhip_sync_info(vrhip_ctx *ctx, uint64_t out[VRHIP_SYNC_INFO]);
 /* Path groups per pixel for vrhip_render in sphere-only scenes (no
  * reference counterpart: a launch shape knob; mesh scenes use the persistent
  * path kernel, whose work queues need none).  A launch of k frames has 2k

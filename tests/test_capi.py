@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(native):
     declared = set(_native.header_symbols())
     assert declared, "no symbols parsed from include/vrhip.h"
     assert declared <= exported, sorted(declared - exported)
-    assert native.vrhip_abi_version() == 5
+    assert native.vrhip_abi_version() == 6
 
 
 def test_build_id_ties_library_to_sources(native):

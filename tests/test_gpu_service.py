@@ -428,3 +428,93 @@ def test_service_scratch_shortage_takes_the_launch_path(native):
     (a0, r0), _, _ = run(0, False)
     assert i1["alloc_fallbacks"] >= 1 and "service" not in k1, (i1, k1)
     _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8")
+
+
+def _one_frame_calls(sc, n, flag, shared=None):
+    """n synchronous one-frame calls (render + vrhip_sync, the reference's
+    cadence) with the completion flag on or off; `shared`: hand the stream or
+    the buffers out first.  Returns the images, the sync counts and the
+    accumulation read between calls."""
+    r = VRendererHIP(0)
+    scenes.load_into(r, sc)
+    r.set_sync_flag(flag)
+    if shared == "stream":
+        r.get_stream()
+    mid = None
+    for i in range(n):
+        r.render(frames=1, times=[sc["time"] + i], sync=True)
+        if shared == "buffers" and i == 0:
+            r.device_buffers()
+        if i == n // 2:
+            mid = r.read_accum()
+    out = r.read_accum(), r.read_rgba8(), r.read_depth8(), r.getFrameCount(), r.sync_info(), mid
+    r.cleanUp()
+    return out
+
+
+@pytest.mark.parametrize("cfg,w,h", [("C2", 160, 96), ("C3", 160, 96), ("C2", 1280, 720)])
+def test_sync_flag_one_frame_calls_equal_stream_sync(native, oracle, cfg, w, h):
+    """vrhip_sync ended by the finish pass's completion flag (the default
+    after a call of one launch): every synchronous call's images equal those
+    of stream-synchronised calls bit for bit, read-backs between calls
+    included, and the 160x96 ones equal the oracle; the flag ends every
+    synchronisation of the flagged context and none of the other."""
+    sc = scenes.make_scene(cfg, w, h)
+    n = 6
+    a1, r1, d1, f1, s1, m1 = _one_frame_calls(sc, n, True)
+    a0, r0, d0, f0, s0, m0 = _one_frame_calls(sc, n, False)
+    assert f1 == f0 == n
+    assert s1["flag"] == n and s0["flag"] == 0 and s0["stream"] >= n
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8"); _eq(d1, d0, "depth8"); _eq(m1, m0, "mid-run accum")
+    if w * h <= 160 * 96:
+        times = [sc["time"] + k for k in range(n)]
+        oa, orgba, od, _ = po.render(sc, frames=n, times=times, libm=po.LIBM_PORTABLE)
+        H, W = (h // 16) * 16, (w // 16) * 16
+        _eq(a1[:H, :W], oa[:H, :W], "accum vs oracle")
+        _eq(r1[:H, :W], orgba[:H, :W], "rgba8 vs oracle")
+
+
+@pytest.mark.parametrize("shared", ["stream", "buffers"])
+def test_sync_flag_off_when_stream_or_buffers_handed_out(native, shared):
+    """A context whose stream or device buffers the caller holds (it may read
+    the images from its own streams) waits for the stream at every sync."""
+    sc = scenes.make_scene("C2", 96, 64)
+    a1, r1, d1, f1, s1, _ = _one_frame_calls(sc, 4, True, shared)
+    a0, r0, d0, f0, s0, _ = _one_frame_calls(sc, 4, False)
+    if shared == "stream":
+        assert s1["flag"] == 0
+    else:
+        assert s1["flag"] <= 1          # the first call's sync precedes the hand-out
+    _eq(a1, a0, "accum"); _eq(r1, r0, "rgba8")
+
+
+def test_sync_flag_multi_frame_and_async_calls(native):
+    """Multi-frame calls, async bursts (the second call overlaps the first on
+    a path stream or the render service), clears and camera moves between
+    synchronisations: images equal the stream-synchronised context's."""
+    sc = scenes.make_scene("C2", 160, 96)
+
+    def run(flag):
+        r = VRendererHIP(0)
+        scenes.load_into(r, sc)
+        r.set_sync_flag(flag)
+        t = sc["time"]
+        outs = []
+        for calls in ([3], [1, 1, 1], [2], [1]):
+            for n in calls:
+                r.render(frames=n, times=[t + k for k in range(n)], sync=False)
+                t += n
+            r.sync()
+            outs.append(r.read_accum())
+        r.clearBuffer()
+        r.render(frames=1, times=[t], sync=True)
+        outs.append(r.read_rgba8())
+        info = r.sync_info()
+        r.cleanUp()
+        return outs, info
+
+    o1, i1 = run(True)
+    o0, _ = run(False)
+    assert i1["flag"] >= 2             # the single-launch calls
+    for k, (x, y) in enumerate(zip(o1, o0)):
+        _eq(x, y, f"step {k}")

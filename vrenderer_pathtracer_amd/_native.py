@@ -94,6 +94,8 @@ _SIGNATURES = {
     "vrhip_last_launch_info": (ctypes.c_int, [_ctx, _u32, _u32, _u32]),
     "vrhip_set_service": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "vrhip_set_kernel_timing": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "vrhip_set_sync_flag": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "vrhip_sync_info": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_uint64)]),
     "vrhip_set_service_timing": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "vrhip_service_stats": (ctypes.c_int, [_ctx, ctypes.POINTER(ctypes.c_uint64)]),
     "vrhip_set_service_budget": (ctypes.c_int, [_ctx, ctypes.c_size_t]),

@@ -15,7 +15,46 @@ namespace vr {
 #ifndef VR_SVC_FINISH_BATCH
 #define VR_SVC_FINISH_BATCH 8
 #endif
+// The completion flag of a synchronous one-frame call (RenderParams::
+// sync_flag): every wave waits for its stores to complete, the block's
+// arrival is counted, and the last block to arrive stores the call's number
+// to host-coherent memory at system scope -- the host sees the frame done
+// without waiting for the stream's completion signal (vrhip_api.cpp one_sync).
+// The results are then complete in the L2s; the end of the kernel writes them
+// back before any later work on the stream starts, and the library arms the
+// flag only on a stream no other party queues work on (vrhip_api.cpp).  (An
+// agent-scope release per wave -- an L2 write-back each -- cost 360 us per
+// 1280x720 finish pass, r06zr.)
+__device__ __forceinline__ void finish_arrive(const RenderParams& p)
+{
+    __builtin_amdgcn_s_waitcnt(0);      // this wave's stores have reached the L2
+    __syncthreads();
+    // two-level count (blocks by blockIdx mod kSyncGroups, then the groups):
+    // the arrivals spread over kSyncGroups words instead of serialising on one
+    // (one word: +25 us per 1280x720 pass, r06zr)
+    if (threadIdx.x == 0) {
+        const uint32_t G = gridDim.x, g = blockIdx.x & (kSyncGroups - 1u);
+        const uint32_t in_group = (G - g + kSyncGroups - 1u) / kSyncGroups, groups = G < kSyncGroups ? G : kSyncGroups;
+        uint32_t* sub = p.sync_ctr + 64u * g;                     // one word per 256 B
+        uint32_t* top = p.sync_ctr + 64u * kSyncGroups;
+        if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1u) {
+            __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1u) {
+                __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(p.sync_flag, p.sync_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void finish_body(const RenderParams& p);
 __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParams p)
+{
+    finish_body(p);
+    if (p.sync_flag) finish_arrive(p);
+}
+
+__device__ __forceinline__ void finish_body(const RenderParams& p)
 {
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
     // the path kernel's queue heads, for the next launch on this scratch

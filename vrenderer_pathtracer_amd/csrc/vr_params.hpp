@@ -156,6 +156,8 @@ struct SvcFinish {
     uint32_t stage_pixels;                         // pixels per staged image (the most any rank owns)
 };
 
+// the finish pass's completion flag: arrival-count groups (a power of two)
+constexpr uint32_t kSyncGroups = 256;
 struct RenderParams {
     vr4 cam_o, cam_d, cx, cy;        // cx, cy precomputed exactly as PathTracer.cu:833-836
     uint32_t W, H, wr, hr;           // wr/hr: rendered region (grid truncation, :888-889)
@@ -224,6 +226,12 @@ struct RenderParams {
     // (8x8 sub-tile) at a time (their count at sparse_count(p), reset by
     // finish_kernel / zeroed when a session opens)
     uint32_t* sparse_px;
+    // a synchronous call's completion flag (nullptr: none): the finish pass's
+    // last block stores sync_seq to host-coherent sync_flag once every block's
+    // results are visible device-wide (sync_ctr: its block counter, left at 0)
+    uint32_t* sync_flag;
+    uint32_t* sync_ctr;              // kSyncGroups group words 256 B apart, then the top word
+    uint32_t sync_seq;
     uint32_t times[kMaxFramesPerLaunch];
 };
 

@@ -235,6 +235,18 @@ struct vrhip_ctx {
     } fgraph[2];
     bool use_graph = false;
     uint64_t graph_launches = 0, graph_captures = 0;
+    // completion flag of a synchronous one-frame call (VRHIP_SYNC_FLAG): the
+    // finish pass's last block stores the call's number to host-coherent
+    // memory, and vrhip_sync polls it instead of waiting for the stream's
+    // completion signal (vr_kernel.hip finish_arrive)
+    int sync_flag_mode = 1;
+    uint32_t* sync_flag = nullptr;   // host-coherent
+    uint32_t* sync_ctr = nullptr;    // device: the finish pass's block arrivals
+    uint32_t sync_seq = 0;
+    uint32_t flag_armed = 0;         // the number the last queued work ends with (0: none)
+    bool flag_synced = false;        // the last sync saw it: no render in flight
+    bool stream_shared = false;      // the caller has the stream (vrhip_get/set_stream): no flag
+    uint64_t sync_flag_waits = 0, sync_stream_waits = 0;
     // the lead of a group: renders since the colour / depth tiles were last
     // gathered (the gather runs when the lead's images are next needed)
     bool group_stale = false;
@@ -246,6 +258,14 @@ struct vrhip_ctx {
     uint32_t comm_rank = 0, comm_n = 0;   // the communicator's rank and size (tiling fixed while it exists)
 };
 
+// the finish pass's arrival counters: vr::kSyncGroups group words 256 B apart, then the top word
+constexpr size_t kSyncCtrBytes = (64u * vr::kSyncGroups + 64u) * sizeof(uint32_t);
+// Largest finish pass that carries the completion flag (tiles of 16x16):
+// counting a 3840x2160 pass's 32,400 block arrivals cost more than the flag
+// saves (C5 one frame per call +0.6 %, r06zt)
+#ifndef VR_SYNC_FLAG_MAX_TILES
+#define VR_SYNC_FLAG_MAX_TILES 8192
+#endif
 static void svc_free(vrhip_ctx* c);
 static int svc_close(vrhip_ctx* c);
 static int refuse_multi(vrhip_ctx* c, const char* what);
@@ -600,6 +620,7 @@ int vrhip_create(int device, uint32_t width, uint32_t height, vrhip_ctx** out)
     if (const char* e = std::getenv("VRHIP_COST_ORDER")) c->cost_order = std::atoi(e) != 0;
     if (const char* e = std::getenv("VRHIP_KERNEL_TIMING")) c->kernel_timing = std::atoi(e) != 0;
     if (const char* e = std::getenv("VRHIP_GRAPH")) c->use_graph = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VRHIP_SYNC_FLAG")) c->sync_flag_mode = std::atoi(e) != 0 ? 1 : 0;
     if (const char* e = std::getenv("VRHIP_SERVICE")) c->service = std::max(-1, std::min(1, std::atoi(e)));
     int rc;
     if ((rc = set_device(c)) != VRHIP_OK) { delete c; return rc; }
@@ -692,6 +713,8 @@ int vrhip_destroy(vrhip_ctx* c)
         if (G.x) (void)hipGraphExecDestroy(G.x);
         if (G.g) (void)hipGraphDestroy(G.g);
     }
+    if (c->sync_flag) (void)hipHostFree(c->sync_flag);
+    dfree(c->sync_ctr);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return VRHIP_OK;
@@ -701,6 +724,7 @@ int vrhip_set_stream(vrhip_ctx* c, void* s)
 {
     if (c && !c->group.empty()) return refuse_multi(c, "vrhip_set_stream");
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    c->stream_shared = true;            // the caller may queue its own work on it: vrhip_sync waits for the stream
     // work queued on the old stream (finish passes) must not reorder with the new one
     if (c->stream && hipSetDevice(c->device) == hipSuccess) {
         (void)svc_close(c);
@@ -711,7 +735,13 @@ int vrhip_set_stream(vrhip_ctx* c, void* s)
     return VRHIP_OK;
 }
 
-void* vrhip_get_stream(vrhip_ctx* c) { return c ? (void*)c->stream : nullptr; }
+void* vrhip_get_stream(vrhip_ctx* c)
+{
+    if (!c) return nullptr;
+    c->stream_shared = true;            // the caller may queue its own work on it: vrhip_sync waits for the stream
+    c->flag_armed = 0;
+    return (void*)c->stream;
+}
 
 static int one_set_camera(vrhip_ctx* c, const float origin[3], const float dir[3], const float up[3],
                      const float right[3], float fov_scale)
@@ -1185,6 +1215,7 @@ static int svc_verify(vrhip_ctx* c)
 static int svc_close(vrhip_ctx* c)
 {
     auto& S = c->svc;
+    c->flag_armed = 0;                  // every call that queues work closes the session first
     if (!S.open) return VRHIP_OK;
     S.open = false;
     __atomic_store_n(&S.host->closed, 1u, __ATOMIC_RELEASE);
@@ -1229,6 +1260,7 @@ static int svc_close(vrhip_ctx* c)
     // vrhip_last_kernel_ms after a session: its span, kernel start to finish pass
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->flag_synced = false;
     // the session's kernel span: one span covering all its launches
     hipEvent_t a = nullptr, b = nullptr;
     if ((a = S.k0) && (b = S.k1)) {
@@ -1458,6 +1490,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     if (!c->cornell && !c->hdr)
         return fail(VRHIP_ERR_NO_ENV, "HDRI mode needs an environment map (vrhip_upload_hdr)");
     int rc = set_device(c); if (rc) return rc;
+    c->flag_armed = 0;
     vr::RenderParams p;
     std::memset(&p, 0, sizeof(p));
     p.cam_o = vr4{ c->cam_o[0], c->cam_o[1], c->cam_o[2], 0.f };
@@ -1521,7 +1554,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     {
         const size_t paths_k = (size_t)p.path_stride * 2u * k_max;
         const bool ovl_size = paths_k < ((size_t)1 << 24) || (c->nranks > 1 && paths_k < ((size_t)1 << 25));
-        const bool in_flight = c->svc.open || (c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
+        const bool in_flight = c->svc.open || (c->timed && !c->flag_synced && hipEventQuery(c->ev1) == hipErrorNotReady);
         // whole frames take the service too: back-to-back launches then
         // overlap each other's drain and share one primary pass (r04 A/B,
         // 16-frame steps, bit-identical: C3 16,505 -> 18,948, C5 21,630 ->
@@ -1610,7 +1643,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
         // previous launch, or the last call's): a launch submitted to an idle
         // device (one frame per synchronous call) runs its render and finish
         // kernels on `stream` with no cross-stream waits
-        const bool in_flight = done > 0 || (c->timed && hipEventQuery(c->ev1) == hipErrorNotReady);
+        const bool in_flight = done > 0 || (c->timed && !c->flag_synced && hipEventQuery(c->ev1) == hipErrorNotReady);
         // counting launches never overlap: their counters are zeroed on
         // `stream` (above), which a path stream would not wait for
         // automatic overlap for launches under 2^24 paths, and under 2^25 for
@@ -1726,8 +1759,28 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
                 HIP_TRY(hipEventRecord(l.done, rs));
                 HIP_TRY(hipStreamWaitEvent(c->stream, l.done, 0));
             }
+            // a call of one launch on `stream` on a context whose stream
+            // nobody else uses: its finish pass is the last work on `stream`,
+            // so it can carry the completion flag a following vrhip_sync polls
+            const bool arm = c->sync_flag_mode && count == 0 && k == n_frames && done == 0 && !on_lane &&
+                             p.use_scratch && n_tiles > 0 && n_tiles <= VR_SYNC_FLAG_MAX_TILES && !c->comm &&
+                             c->group.empty() && !c->stream_shared;
+            if (arm) {
+                if (!c->sync_flag) {
+                    HIP_TRY(hipHostMalloc((void**)&c->sync_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+                    *c->sync_flag = 0u;
+                }
+                if (!c->sync_ctr) {
+                    HIP_TRY(hipMalloc((void**)&c->sync_ctr, kSyncCtrBytes));
+                    HIP_TRY(hipMemsetAsync(c->sync_ctr, 0, kSyncCtrBytes, c->stream));
+                }
+                if (++c->sync_seq == 0u) c->sync_seq = 1u;
+                p.sync_flag = c->sync_flag; p.sync_ctr = c->sync_ctr; p.sync_seq = c->sync_seq;
+            }
             e = vr::launch_finish(p, n_tiles, c->stream);
             if (e != 0) return fail(VRHIP_ERR_HIP, std::string("finish launch: ") + hipGetErrorString((hipError_t)e));
+            if (arm) c->flag_armed = p.sync_seq;
+            p.sync_flag = nullptr; p.sync_ctr = nullptr;
         }
         int e = 0;
         if (p.use_scratch) {
@@ -1753,6 +1806,7 @@ static int render_impl(vrhip_ctx* c, uint32_t n_frames, const uint32_t* times, u
     }
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->flag_synced = false;
     // kernel-time accounting of launches already completed: after this call's
     // launches are queued, so its event queries do not delay them (one frame
     // per synchronous call: they sat between the host's wake-up and the launch)
@@ -1872,13 +1926,58 @@ int vrhip_last_launch_info(vrhip_ctx* c, uint32_t* split, uint32_t* use_scratch,
     return VRHIP_OK;
 }
 
+// Waits until the finish pass armed with number `seq` (render_impl) has
+// stored it: the host sees the frame complete without the ≈ 13 µs the
+// stream's completion signal takes after the kernel (profiles/r06i).  A
+// fault or failed launch is caught by the hipStreamQuery made every ≈ 30 µs.
+static int wait_flag(vrhip_ctx* c, uint32_t seq)
+{
+    ++c->sync_flag_waits;
+    for (uint32_t n = 1;; ++n) {
+        if (__atomic_load_n(c->sync_flag, __ATOMIC_ACQUIRE) == seq) break;
+        if ((n & 1023u) == 0u) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e == hipSuccess) break;                    // drained (the flag is set too)
+            if (e != hipErrorNotReady) return fail(VRHIP_ERR_HIP, std::string("sync: ") + hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+    c->flag_synced = true;
+    return VRHIP_OK;
+}
+
 static int one_sync(vrhip_ctx* c)
 {
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     int rc = set_device(c); if (rc) return rc;
+    const uint32_t armed = c->svc.open ? 0u : c->flag_armed;
     if ((rc = svc_close(c)) != VRHIP_OK) return rc;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (armed) {
+        if ((rc = wait_flag(c, armed)) != VRHIP_OK) return rc;
+    } else {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        ++c->sync_stream_waits;
+    }
     return svc_verify(c);
+}
+
+static int one_set_sync_flag(vrhip_ctx* c, int on)
+{
+    if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
+    c->sync_flag_mode = on != 0 ? 1 : 0;
+    c->flag_armed = 0;
+    return VRHIP_OK;
+}
+
+int vrhip_sync_info(vrhip_ctx* c, uint64_t out[VRHIP_SYNC_INFO])
+{
+    if (!c || !out) return fail(VRHIP_ERR_INVALID, "null argument");
+    uint64_t a = 0, b = 0;
+    for (vrhip_ctx* m : c->group.empty() ? std::vector<vrhip_ctx*>{ c } : c->group) {
+        a += m->sync_flag_waits; b += m->sync_stream_waits;
+    }
+    out[0] = a; out[1] = b;
+    return VRHIP_OK;
 }
 
 int vrhip_frame_count(vrhip_ctx* c, uint32_t* frames)
@@ -1925,6 +2024,9 @@ int vrhip_device_buffers(vrhip_ctx* c, void** accum, void** rgba8, void** depth8
     if (!c) return fail(VRHIP_ERR_INVALID, "null ctx");
     const int rc = multi_images(c); if (rc) return rc;       // a group's lead: the whole image first
     if (set_device(c) == VRHIP_OK) (void)svc_close(c);     // the buffers hold every render so far
+    // the caller may read them from its own streams: vrhip_sync then waits
+    // for the stream's completion (the end of the kernels' write-back)
+    c->stream_shared = true;
     if (accum) *accum = c->accum;
     if (rgba8) *rgba8 = c->rgba;
     if (depth8) *depth8 = c->depth;
@@ -2429,6 +2531,7 @@ int vrhip_set_overlap(vrhip_ctx* c, int mode) { return fanout(c, [&](vrhip_ctx* 
 int vrhip_set_path_split(vrhip_ctx* c, uint32_t groups) { return fanout(c, [&](vrhip_ctx* m) { return one_set_path_split(m, groups); }); }
 int vrhip_set_service(vrhip_ctx* c, int mode) { return fanout(c, [&](vrhip_ctx* m) { return one_set_service(m, mode); }); }
 int vrhip_set_kernel_timing(vrhip_ctx* c, int on) { return fanout(c, [&](vrhip_ctx* m) { return one_set_kernel_timing(m, on); }); }
+int vrhip_set_sync_flag(vrhip_ctx* c, int on) { return fanout(c, [&](vrhip_ctx* m) { return one_set_sync_flag(m, on); }); }
 int vrhip_sync(vrhip_ctx* c)
 {
     const int rc = multi_images(c);                  // a group: the lead's images are complete after a sync

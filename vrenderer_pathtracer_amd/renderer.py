@@ -365,6 +365,17 @@ class VRendererHIP:
         synchronous one-frame call)."""
         check(self._lib.vrhip_set_kernel_timing(self._need_ctx(), int(bool(on))), "vrhip_set_kernel_timing")
 
+    def set_sync_flag(self, on: bool) -> None:
+        """vrhip_sync by the finish pass's completion flag after one-launch
+        calls (vrhip_set_sync_flag; on by default)."""
+        check(self._lib.vrhip_set_sync_flag(self._need_ctx(), int(bool(on))), "vrhip_set_sync_flag")
+
+    def sync_info(self) -> dict:
+        """Synchronisations since creation, by how they ended (vrhip_sync_info)."""
+        c = (ctypes.c_uint64 * 2)()
+        check(self._lib.vrhip_sync_info(self._need_ctx(), c), "vrhip_sync_info")
+        return {"flag": int(c[0]), "stream": int(c[1])}
+
     def set_service_timing(self, idle_us: int = 0, post_window_us: int = 0, post_delay_us: int = 0) -> None:
         """Test hook (vrhip_set_service_timing): the session kernel's idle
         limit, the host's post window and a host delay before each post
