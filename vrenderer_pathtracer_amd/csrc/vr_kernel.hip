@@ -47,14 +47,27 @@ __device__ __forceinline__ void finish_arrive(const RenderParams& p)
     }
 }
 
-__device__ __forceinline__ void finish_body(const RenderParams& p);
+__device__ __forceinline__ void finish_body(const RenderParams& p, const float* T);
+#ifndef VR_FINISH_LDS_TONE
+#define VR_FINISH_LDS_TONE 1
+#endif
 __global__ void __launch_bounds__(kBlockThreads) finish_kernel(const RenderParams p)
 {
-    finish_body(p);
+#if VR_FINISH_LDS_TONE
+    // the tonemap's 256 thresholds in LDS: the dependent table reads of each
+    // colour byte (tone_byte) then wait on LDS instead of the L1
+    static_assert(kBlockThreads == 256, "one threshold per thread");
+    __shared__ float T[256];
+    T[threadIdx.x] = p.tone_t ? p.tone_t[threadIdx.x] : 0.f;
+    __syncthreads();
+    finish_body(p, p.tone_t ? T : nullptr);
+#else
+    finish_body(p, p.tone_t);
+#endif
     if (p.sync_flag) finish_arrive(p);
 }
 
-__device__ __forceinline__ void finish_body(const RenderParams& p)
+__device__ __forceinline__ void finish_body(const RenderParams& p, const float* T)
 {
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
     // the path kernel's queue heads, for the next launch on this scratch
@@ -104,7 +117,7 @@ __device__ __forceinline__ void finish_body(const RenderParams& p)
     const unsigned char db = f2u8((1.f - last_w) * 255);
     u8x4 dv; dv.x = db; dv.y = db; dv.z = db; dv.w = 0xff;
     p.depth[ind] = dv;
-    p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u, p.tone_t);
+    p.rgba[ind] = tonemap(io, p.first_frame + p.n_frames - 1u, T);
     p.accum[ind] = io;
     if (p.path_cost) {
         // the sub-tile's cost for the next launch's order: its paths' costs,
